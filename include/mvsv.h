@@ -1,0 +1,202 @@
+/*
+ * mvsv.h — C ABI of the MI355X-native stereo disparity engine (libmvsv.so).
+ *
+ * This is the drop-in boundary for the reference's disparity hot path.  Every
+ * entry point replaces one reference interface (hG3n/mvStereoVision3):
+ *
+ *   mvsv_sgbm / mvsv_sgbm_device      Disparity::sgbm        src/disparity.cpp:6-10,
+ *                                     decl inc/disparity.h:29 (forwards to
+ *                                     cv::StereoSGBM::compute, also called
+ *                                     directly at trgt/liveDisparity.cpp:91)
+ *   mvsv_bm / mvsv_bm_device          Disparity::bm          src/disparity.cpp:18-22,
+ *                                     decl inc/disparity.h:31
+ *   mvsv_load_sgbm_yaml               Disparity::loadSGBMParameters
+ *                                     src/disparity.cpp:60-108, inc/disparity.h:34
+ *   mvsv_load_bm_yaml                 (new) loader for configs/bm.yml:2-7, which
+ *                                     the reference ships but never reads
+ *   mvsv_sgbm_params / mvsv_bm_params cv::StereoSGBM / cv::StereoBM state set by
+ *                                     create() + setters (src/disparity.cpp:83-95,
+ *                                     trgt/liveDisparity.cpp:61); field meaning and
+ *                                     defaults are OpenCV 3.4's
+ *   mvsv_sgbm_yaml_values             struct Disparity::sgbmParameters
+ *                                     inc/disparity.h:17-27
+ *   mvsv_mean_disparity_grid_device   MeanDisparityDetection::build(MEAN_VALUE)
+ *                                     src/MeanDisparityDetection.cpp:159-206 +
+ *                                     Utility::calcMeanDisparity src/utility.cpp:265-285
+ *
+ * Conventions
+ *   - Plain C types only; no exceptions cross this boundary.
+ *   - Every function returns MVSV_OK (0) or a negative MVSV_E_* code; the
+ *     context's message is available through mvsv_last_error().
+ *   - Parameter validation follows OpenCV's CV_Assert/CV_Error rules for the
+ *     same call (invalid -> MVSV_E_INVALID_ARG instead of cv::Exception).
+ *   - Output is CV_16S-compatible: int16 disparity * 16 (DISP_SHIFT = 4);
+ *     invalid pixels are (minDisparity - 1) * 16.
+ *   - A context owns one HIP stream and its cached device buffers; it is not
+ *     thread-safe: use one context per host thread (the reference runs one
+ *     matcher per worker thread, trgt/mean_test.cpp:61-70).
+ *   - Host-pointer calls (mvsv_sgbm, mvsv_bm) are synchronous.  Device-pointer
+ *     calls (*_device) enqueue on the context stream and return immediately;
+ *     call mvsv_synchronize() before reading results on the host.
+ */
+#ifndef MVSV_H
+#define MVSV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__GNUC__)
+#define MVSV_API __attribute__((visibility("default")))
+#else
+#define MVSV_API
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MVSV_VERSION 100 /* 1.0.0 */
+
+enum {
+    MVSV_OK = 0,
+    MVSV_E_INVALID_ARG = -1, /* OpenCV would throw cv::Exception (StsOutOfRange / assert) */
+    MVSV_E_HIP = -2,         /* HIP runtime error (launch, copy, device) */
+    MVSV_E_OOM = -3,         /* device or host allocation failed */
+    MVSV_E_IO = -4,          /* cannot open file */
+    MVSV_E_PARSE = -5,       /* missing / malformed YAML key */
+    MVSV_E_NODEV = -6        /* no HIP device available */
+};
+
+/* StereoSGBM modes (cv::StereoSGBM::MODE_SGBM / MODE_HH). */
+enum { MVSV_MODE_SGBM = 0, MVSV_MODE_HH = 1 };
+/* StereoBM prefilter types (cv::StereoBM::PREFILTER_*). */
+enum { MVSV_PREFILTER_NORMALIZED_RESPONSE = 0, MVSV_PREFILTER_XSOBEL = 1 };
+
+/* Semantic variants of OpenCV releases (bit flags in mvsv_sgbm_params.variant).
+ * 0 = OpenCV 3.4.x CV_SIMD128 behaviour (the pinned default). */
+enum {
+    MVSV_VARIANT_FIRSTCOL_FIX = 1, /* later releases refresh cost column x=0 */
+    MVSV_VARIANT_WTA_MIN_D = 2     /* later releases: MODE_SGBM ties -> smallest d */
+};
+
+typedef struct {
+    int min_disparity;       /* setMinDisparity */
+    int num_disparities;     /* setNumDisparities, must be > 0 and % 16 == 0 */
+    int block_size;          /* setBlockSize (<= 0 -> 5) */
+    int p1, p2;              /* setP1 / setP2 (<= 0 -> 2 / 5, P2 = max(P2, P1+1)) */
+    int disp12_max_diff;     /* setDisp12MaxDiff (<= 0 -> 1) */
+    int pre_filter_cap;      /* setPreFilterCap (ftzero = max(cap,15)|1) */
+    int uniqueness_ratio;    /* setUniquenessRatio (< 0 -> 10) */
+    int speckle_window_size; /* setSpeckleWindowSize (0 disables speckle filter) */
+    int speckle_range;       /* setSpeckleRange (multiplied by 16) */
+    int mode;                /* MVSV_MODE_SGBM (5 paths) or MVSV_MODE_HH (8 paths) */
+    int variant;             /* MVSV_VARIANT_* bits, 0 = OpenCV 3.4 */
+} mvsv_sgbm_params;
+
+typedef struct {
+    int pre_filter_type;     /* MVSV_PREFILTER_XSOBEL (default) or _NORMALIZED_RESPONSE */
+    int pre_filter_size;     /* odd, 5..255 */
+    int pre_filter_cap;      /* 1..63 */
+    int block_size;          /* odd, 5..255, < min(W, H) */
+    int min_disparity;
+    int num_disparities;     /* > 0, % 16 == 0 */
+    int texture_threshold;   /* >= 0 */
+    int uniqueness_ratio;    /* >= 0 */
+    int speckle_window_size;
+    int speckle_range;
+    int disp12_max_diff;     /* < 0 disables the left-right check */
+} mvsv_bm_params;
+
+/* Disparity::sgbmParameters (inc/disparity.h:17-27): the raw YAML values. */
+typedef struct {
+    int minDisp, numDisp, blockSize, disp12MaxDiff, preFilterCap, uniquenessRatio,
+        speckleWindowSize, speckleRange, disparityMode;
+} mvsv_sgbm_yaml_values;
+
+typedef struct mvsv_ctx mvsv_ctx;
+
+MVSV_API int mvsv_version(void);
+
+/* StereoSGBM::create() defaults: (0, 16, 3, 0, 0, 0, 0, 0, 0, 0, MODE_SGBM). */
+MVSV_API void mvsv_sgbm_params_default(mvsv_sgbm_params* p);
+/* StereoSGBM::create(minDisparity, numDisparities, blockSize, P1, P2, ...). */
+MVSV_API void mvsv_sgbm_params_create(mvsv_sgbm_params* p, int min_disparity,
+                                      int num_disparities, int block_size, int p1, int p2,
+                                      int disp12_max_diff, int pre_filter_cap,
+                                      int uniqueness_ratio, int speckle_window_size,
+                                      int speckle_range, int mode);
+/* StereoBM::create(numDisparities, blockSize) defaults. */
+MVSV_API void mvsv_bm_params_default(mvsv_bm_params* p, int num_disparities, int block_size);
+
+/* Validation only (no device needed): MVSV_OK or MVSV_E_INVALID_ARG. */
+MVSV_API int mvsv_sgbm_validate(const mvsv_sgbm_params* p, int W, int H);
+MVSV_API int mvsv_bm_validate(const mvsv_bm_params* p, int W, int H);
+
+MVSV_API int mvsv_create(mvsv_ctx** out, int hip_device);
+MVSV_API void mvsv_destroy(mvsv_ctx* ctx);
+MVSV_API const char* mvsv_last_error(const mvsv_ctx* ctx);
+/* Use an external hipStream_t (e.g. the caller's current stream); NULL restores
+ * the context's own stream. */
+MVSV_API int mvsv_set_stream(mvsv_ctx* ctx, void* hip_stream);
+MVSV_API void* mvsv_get_stream(mvsv_ctx* ctx);
+MVSV_API int mvsv_synchronize(mvsv_ctx* ctx);
+/* Release cached device buffers. */
+MVSV_API int mvsv_trim(mvsv_ctx* ctx);
+
+/* Host pointers, synchronous.  Strides are in elements (bytes for u8, int16
+ * elements for out); stride >= W allows ROI views (src/Stereosystem.cpp:255-256). */
+MVSV_API int mvsv_sgbm(mvsv_ctx* ctx, const uint8_t* left, size_t left_stride,
+                       const uint8_t* right, size_t right_stride, int width, int height,
+                       const mvsv_sgbm_params* p, int16_t* out, size_t out_stride);
+MVSV_API int mvsv_bm(mvsv_ctx* ctx, const uint8_t* left, size_t left_stride,
+                     const uint8_t* right, size_t right_stride, int width, int height,
+                     const mvsv_bm_params* p, int16_t* out, size_t out_stride);
+
+/* Device pointers (HBM-resident), asynchronous on the context stream.
+ * A batch of n frames: frame i starts at base + i * frame_stride (elements). */
+MVSV_API int mvsv_sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* left, size_t left_stride,
+                              size_t left_frame_stride, const uint8_t* right,
+                              size_t right_stride, size_t right_frame_stride, int width,
+                              int height, const mvsv_sgbm_params* p, int16_t* out,
+                              size_t out_stride, size_t out_frame_stride);
+MVSV_API int mvsv_bm_device(mvsv_ctx* ctx, int n, const uint8_t* left, size_t left_stride,
+                            size_t left_frame_stride, const uint8_t* right,
+                            size_t right_stride, size_t right_frame_stride, int width,
+                            int height, const mvsv_bm_params* p, int16_t* out,
+                            size_t out_stride, size_t out_frame_stride);
+
+/* Device bytes the context will cache for one SGBM / BM call of this shape. */
+MVSV_API size_t mvsv_sgbm_workspace_bytes(int n, int width, int height,
+                                          const mvsv_sgbm_params* p);
+
+/* MeanDisparityDetection post-pass on device: 9x9 tile means of an int16 map
+ * (tile = (W/9)x(H/9), remainder ignored; mean over values > 1 with integer
+ * division, 0 for an empty tile).  means: 81 floats per frame (device ptr). */
+MVSV_API int mvsv_mean_disparity_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap,
+                                             size_t stride, size_t frame_stride, int width,
+                                             int height, float* means);
+
+/* Disparity::loadSGBMParameters: reads configs/sgbm.yml keys minDisp, numDisp,
+ * blockSize, disp12MaxDiff, preFilterCap, uniquenessRatio, speckleWindowSize,
+ * speckleWindowRange, mode into *values and applies the 8 setters + mode to
+ * *p (P1/P2 untouched, as in the reference).  Missing numDisp, blockSize,
+ * speckleWindowSize or speckleWindowRange -> MVSV_E_PARSE; other keys missing
+ * leave the value 0 (cv::FileNode >> int on an empty node). */
+MVSV_API int mvsv_load_sgbm_yaml(const char* path, mvsv_sgbm_params* p,
+                                 mvsv_sgbm_yaml_values* values);
+/* configs/bm.yml keys: numDisp, blockSize, preFilterCap, preFilterSize,
+ * uniquenessRatio, textureThreshold (+ optional minDisp, speckleWindowSize,
+ * speckleWindowRange, disp12MaxDiff, preFilterType). numDisp and blockSize are
+ * required. */
+MVSV_API int mvsv_load_bm_yaml(const char* path, mvsv_bm_params* p);
+
+/* Deterministic synthetic rectified pair: PCG32 noise,
+ * 3x3 box blur, slanted-plane + rectangle disparity field, +-1 noise.
+ * Host buffers of width*height bytes each. */
+MVSV_API int mvsv_synth_pair(uint32_t seed, int width, int height, int min_disparity,
+                             int num_disparities, uint8_t* left, uint8_t* right);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MVSV_H */

@@ -1,0 +1,19 @@
+"""mvstereovision3_amd — MI355X-native stereo disparity engine.
+
+Drop-in for the disparity hot path of hG3n/mvStereoVision3
+(Disparity::sgbm / Disparity::bm / Disparity::loadSGBMParameters,
+src/disparity.cpp:6-108).  Compute lives in hand-written HIP kernels for
+gfx950 behind the C ABI of libmvsv.so (include/mvsv.h); this package is the
+host-side mirror of the reference interface.
+"""
+from ._lib import (MODE_HH, MODE_SGBM, PREFILTER_NORMALIZED_RESPONSE, PREFILTER_XSOBEL,
+                   VARIANT_FIRSTCOL_FIX, VARIANT_WTA_MIN_D, MvsvError)
+from .disparity import (Disparity, StereoBM, StereoSGBM, Stereopair, mean_disparity_grid,
+                        sgbmParameters, synth_pair)
+
+__all__ = [
+    "Disparity", "StereoBM", "StereoSGBM", "Stereopair", "sgbmParameters", "MvsvError",
+    "synth_pair", "mean_disparity_grid", "MODE_SGBM", "MODE_HH", "PREFILTER_XSOBEL",
+    "PREFILTER_NORMALIZED_RESPONSE", "VARIANT_FIRSTCOL_FIX", "VARIANT_WTA_MIN_D",
+]
+__version__ = "1.0.0"

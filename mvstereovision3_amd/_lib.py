@@ -1,0 +1,177 @@
+"""ctypes binding of libmvsv.so (the C ABI declared in include/mvsv.h).
+
+The library is built in-tree by ``__graft_entry__.build()``
+(mvstereovision3_amd/csrc/Makefile -> mvstereovision3_amd/libmvsv.so).  There
+is no fallback: if the library is missing, every entry point raises
+:class:`MvsvError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmvsv.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mvsv.h")
+
+MVSV_OK = 0
+MVSV_E_INVALID_ARG = -1
+MVSV_E_HIP = -2
+MVSV_E_OOM = -3
+MVSV_E_IO = -4
+MVSV_E_PARSE = -5
+MVSV_E_NODEV = -6
+
+MODE_SGBM = 0
+MODE_HH = 1
+PREFILTER_NORMALIZED_RESPONSE = 0
+PREFILTER_XSOBEL = 1
+VARIANT_FIRSTCOL_FIX = 1
+VARIANT_WTA_MIN_D = 2
+
+_CODES = {
+    MVSV_E_INVALID_ARG: "invalid argument",
+    MVSV_E_HIP: "HIP error",
+    MVSV_E_OOM: "out of memory",
+    MVSV_E_IO: "cannot open file",
+    MVSV_E_PARSE: "missing or malformed key",
+    MVSV_E_NODEV: "no HIP device",
+}
+
+
+class MvsvError(RuntimeError):
+    """Raised for every negative MVSV_E_* code (OpenCV would throw cv::Exception)."""
+
+    def __init__(self, code: int, msg: str = ""):
+        self.code = code
+        super().__init__(f"mvsv error {code} ({_CODES.get(code, 'unknown')}){': ' + msg if msg else ''}")
+
+
+SGBM_FIELDS = ("min_disparity", "num_disparities", "block_size", "p1", "p2",
+               "disp12_max_diff", "pre_filter_cap", "uniqueness_ratio",
+               "speckle_window_size", "speckle_range", "mode", "variant")
+BM_FIELDS = ("pre_filter_type", "pre_filter_size", "pre_filter_cap", "block_size",
+             "min_disparity", "num_disparities", "texture_threshold", "uniqueness_ratio",
+             "speckle_window_size", "speckle_range", "disp12_max_diff")
+YAML_FIELDS = ("minDisp", "numDisp", "blockSize", "disp12MaxDiff", "preFilterCap",
+               "uniquenessRatio", "speckleWindowSize", "speckleRange", "disparityMode")
+
+
+class SgbmParams(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_int) for f in SGBM_FIELDS]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f in SGBM_FIELDS}
+
+
+class BmParams(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_int) for f in BM_FIELDS]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f in BM_FIELDS}
+
+
+class SgbmYamlValues(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_int) for f in YAML_FIELDS]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _declare(lib):
+    P = ctypes.c_void_p
+    I = ctypes.c_int
+    Z = ctypes.c_size_t
+    sig = {
+        "mvsv_version": ([], I),
+        "mvsv_sgbm_params_default": ([P], None),
+        "mvsv_sgbm_params_create": ([P] + [I] * 11, None),
+        "mvsv_bm_params_default": ([P, I, I], None),
+        "mvsv_sgbm_validate": ([P, I, I], I),
+        "mvsv_bm_validate": ([P, I, I], I),
+        "mvsv_create": ([ctypes.POINTER(P), I], I),
+        "mvsv_destroy": ([P], None),
+        "mvsv_last_error": ([P], ctypes.c_char_p),
+        "mvsv_set_stream": ([P, P], I),
+        "mvsv_get_stream": ([P], P),
+        "mvsv_synchronize": ([P], I),
+        "mvsv_trim": ([P], I),
+        "mvsv_sgbm": ([P, P, Z, P, Z, I, I, P, P, Z], I),
+        "mvsv_bm": ([P, P, Z, P, Z, I, I, P, P, Z], I),
+        "mvsv_sgbm_device": ([P, I, P, Z, Z, P, Z, Z, I, I, P, P, Z, Z], I),
+        "mvsv_bm_device": ([P, I, P, Z, Z, P, Z, Z, I, I, P, P, Z, Z], I),
+        "mvsv_sgbm_workspace_bytes": ([I, I, I, P], Z),
+        "mvsv_mean_disparity_grid_device": ([P, I, P, Z, Z, I, I, P], I),
+        "mvsv_load_sgbm_yaml": ([ctypes.c_char_p, P, P], I),
+        "mvsv_load_bm_yaml": ([ctypes.c_char_p, P], I),
+        "mvsv_synth_pair": ([ctypes.c_uint32, I, I, I, I, P, P], I),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib
+
+
+def lib():
+    """Load libmvsv.so (torch first, so both share one HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            try:  # torch bundles libamdhip64.so.7; load it first so the SONAME is shared
+                import torch  # noqa: F401
+            except ImportError:  # pragma: no cover - torch is always present in this image
+                pass
+            if not os.path.exists(LIB_PATH):
+                raise MvsvError(MVSV_E_INVALID_ARG,
+                                f"{LIB_PATH} is not built; run __graft_entry__.build()")
+            _lib = _declare(ctypes.CDLL(LIB_PATH))
+    return _lib
+
+
+def check(rc: int, ctx=None) -> int:
+    if rc < 0:
+        msg = ""
+        if ctx:
+            raw = lib().mvsv_last_error(ctx)
+            msg = raw.decode() if raw else ""
+        raise MvsvError(rc, msg)
+    return rc
+
+
+class Context:
+    """One mvsv_ctx (HIP stream + cached device buffers) per device and thread."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        h = ctypes.c_void_p()
+        check(lib().mvsv_create(ctypes.byref(h), device))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            lib().mvsv_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_tls = threading.local()
+
+
+def context(device: int = 0) -> Context:
+    ctxs = getattr(_tls, "ctxs", None)
+    if ctxs is None:
+        ctxs = _tls.ctxs = {}
+    c = ctxs.get(device)
+    if c is None:
+        c = ctxs[device] = Context(device)
+    return c

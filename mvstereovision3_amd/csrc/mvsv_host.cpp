@@ -1,0 +1,535 @@
+// mvsv_host.cpp — host side of libmvsv: parameter resolution (OpenCV's
+// defaulting + assert rules), context / stream / buffer management, the
+// host-pointer entry points, the YAML loaders and the synthetic generator.
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+
+#include "mvsv_internal.hpp"
+
+namespace mvsv {
+
+int set_error(mvsv_ctx* ctx, int code, const std::string& msg)
+{
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+int check_hip(mvsv_ctx* ctx, hipError_t e, const char* what)
+{
+    if (e == hipSuccess) return MVSV_OK;
+    return set_error(ctx, e == hipErrorOutOfMemory ? MVSV_E_OOM : MVSV_E_HIP,
+                     std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int ensure(mvsv_ctx* ctx, DevBuf& b, size_t bytes, const char* what)
+{
+    if (bytes <= b.bytes && b.ptr) return MVSV_OK;
+    if (b.ptr) {
+        // the stream may still use the old buffer
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(b.ptr);
+        b.ptr = nullptr;
+        b.bytes = 0;
+    }
+    if (bytes == 0) return MVSV_OK;
+    hipError_t e = hipMalloc(&b.ptr, bytes);
+    if (e != hipSuccess) {
+        b.ptr = nullptr;
+        (void)hipGetLastError();
+        return set_error(ctx, MVSV_E_OOM,
+                         std::string("device allocation of ") + std::to_string(bytes) +
+                             " bytes for " + what + " failed");
+    }
+    b.bytes = bytes;
+    return MVSV_OK;
+}
+
+// [OpenCV] StereoSGBMImpl::compute asserts + computeDisparitySGBM prologue.
+int resolve_sgbm(const mvsv_sgbm_params* p, int W, int H, SgbmEff* e, std::string* why)
+{
+    if (!p) { *why = "null parameters"; return MVSV_E_INVALID_ARG; }
+    if (W <= 0 || H <= 0) { *why = "empty image"; return MVSV_E_INVALID_ARG; }
+    if (p->num_disparities <= 0 || p->num_disparities % 16 != 0) {
+        *why = "numDisparities must be positive and divisible by 16";
+        return MVSV_E_INVALID_ARG;
+    }
+    if (p->mode != MVSV_MODE_SGBM && p->mode != MVSV_MODE_HH) {
+        *why = "mode must be MODE_SGBM (0) or MODE_HH (1)";
+        return MVSV_E_INVALID_ARG;
+    }
+    int bs = p->block_size > 0 ? p->block_size : 5;
+    e->minD = p->min_disparity;
+    e->D = p->num_disparities;
+    e->maxD = e->minD + e->D;
+    e->SW2 = bs / 2;
+    e->SH2 = bs / 2;
+    e->ftzero = std::max(p->pre_filter_cap, 15) | 1;
+    e->uniq = p->uniqueness_ratio >= 0 ? p->uniqueness_ratio : 10;
+    e->disp12 = p->disp12_max_diff > 0 ? p->disp12_max_diff : 1;
+    e->P1 = p->p1 > 0 ? p->p1 : 2;
+    e->P2 = std::max(p->p2 > 0 ? p->p2 : 5, e->P1 + 1);
+    e->minX1 = std::max(e->maxD, 0);
+    e->maxX1 = W + std::min(e->minD, 0);
+    e->W1 = e->maxX1 - e->minX1;
+    e->invalid = (e->minD - 1) * kDispScale;
+    e->fullDP = p->mode == MVSV_MODE_HH;
+    e->variant = p->variant;
+    e->speckle_window = p->speckle_window_size;
+    e->speckle_diff = kDispScale * p->speckle_range;
+    if (e->W1 > 0 && e->W1 <= e->SW2) {
+        *why = "image narrower than the SGBM block half-width (OpenCV reads uninitialised memory)";
+        return MVSV_E_INVALID_ARG;
+    }
+    return MVSV_OK;
+}
+
+// [OpenCV] StereoBMImpl::compute checks + findStereoCorrespondenceBM setup.
+int resolve_bm(const mvsv_bm_params* p, int W, int H, BmEff* e, std::string* why)
+{
+    if (!p) { *why = "null parameters"; return MVSV_E_INVALID_ARG; }
+    if (W <= 0 || H <= 0) { *why = "empty image"; return MVSV_E_INVALID_ARG; }
+    if (p->pre_filter_type != MVSV_PREFILTER_NORMALIZED_RESPONSE &&
+        p->pre_filter_type != MVSV_PREFILTER_XSOBEL) {
+        *why = "preFilterType must be = CV_STEREO_BM_NORMALIZED_RESPONSE";
+        return MVSV_E_INVALID_ARG;
+    }
+    if (p->pre_filter_size < 5 || p->pre_filter_size > 255 || p->pre_filter_size % 2 == 0) {
+        *why = "preFilterSize must be odd and be within 5..255";
+        return MVSV_E_INVALID_ARG;
+    }
+    if (p->pre_filter_cap < 1 || p->pre_filter_cap > 63) {
+        *why = "preFilterCap must be within 1..63";
+        return MVSV_E_INVALID_ARG;
+    }
+    if (p->block_size < 5 || p->block_size > 255 || p->block_size % 2 == 0 ||
+        p->block_size >= std::min(W, H)) {
+        *why = "SADWindowSize must be odd, be within 5..255 and be not larger than image width or height";
+        return MVSV_E_INVALID_ARG;
+    }
+    if (p->num_disparities <= 0 || p->num_disparities % 16 != 0) {
+        *why = "numDisparities must be positive and divisible by 16";
+        return MVSV_E_INVALID_ARG;
+    }
+    if (p->texture_threshold < 0) { *why = "texture threshold must be non-negative"; return MVSV_E_INVALID_ARG; }
+    if (p->uniqueness_ratio < 0) { *why = "uniqueness ratio must be non-negative"; return MVSV_E_INVALID_ARG; }
+    e->ndisp = p->num_disparities;
+    e->mindisp = p->min_disparity;
+    e->wsz2 = p->block_size / 2;
+    e->cap = p->pre_filter_cap;
+    e->tex = p->texture_threshold;
+    e->uniq = p->uniqueness_ratio;
+    e->lofs = std::max(e->ndisp - 1 + e->mindisp, 0);
+    e->rofs = -std::min(e->ndisp - 1 + e->mindisp, 0);
+    e->width1 = W - e->rofs - e->ndisp + 1;
+    e->ncol = std::min(e->width1, W - e->lofs);
+    e->filtered = (e->mindisp - 1) * kDispScale;
+    int maxDm1 = e->mindisp + e->ndisp - 1;
+    e->xmin = std::max(0, maxDm1) + e->wsz2;
+    e->xmax = W - e->wsz2;
+    e->ymin = e->wsz2;
+    e->ymax = H - e->wsz2;
+    e->disp12 = p->disp12_max_diff;
+    e->speckle_window = p->speckle_window_size;
+    e->speckle_range = p->speckle_range;
+    e->prefilter_type = p->pre_filter_type;
+    e->prefilter_size = p->pre_filter_size;
+    return MVSV_OK;
+}
+
+}  // namespace mvsv
+
+using namespace mvsv;
+
+extern "C" {
+
+int mvsv_version(void) { return MVSV_VERSION; }
+
+void mvsv_sgbm_params_create(mvsv_sgbm_params* p, int min_disparity, int num_disparities,
+                             int block_size, int p1, int p2, int disp12_max_diff,
+                             int pre_filter_cap, int uniqueness_ratio, int speckle_window_size,
+                             int speckle_range, int mode)
+{
+    if (!p) return;
+    p->min_disparity = min_disparity;
+    p->num_disparities = num_disparities;
+    p->block_size = block_size;
+    p->p1 = p1;
+    p->p2 = p2;
+    p->disp12_max_diff = disp12_max_diff;
+    p->pre_filter_cap = pre_filter_cap;
+    p->uniqueness_ratio = uniqueness_ratio;
+    p->speckle_window_size = speckle_window_size;
+    p->speckle_range = speckle_range;
+    p->mode = mode;
+    p->variant = 0;
+}
+
+void mvsv_sgbm_params_default(mvsv_sgbm_params* p)
+{
+    mvsv_sgbm_params_create(p, 0, 16, 3, 0, 0, 0, 0, 0, 0, 0, MVSV_MODE_SGBM);
+}
+
+void mvsv_bm_params_default(mvsv_bm_params* p, int num_disparities, int block_size)
+{
+    if (!p) return;
+    p->pre_filter_type = MVSV_PREFILTER_XSOBEL;
+    p->pre_filter_size = 9;
+    p->pre_filter_cap = 31;
+    p->block_size = block_size;
+    p->min_disparity = 0;
+    p->num_disparities = num_disparities > 0 ? num_disparities : 64;
+    p->texture_threshold = 10;
+    p->uniqueness_ratio = 15;
+    p->speckle_window_size = 0;
+    p->speckle_range = 0;
+    p->disp12_max_diff = -1;
+}
+
+int mvsv_sgbm_validate(const mvsv_sgbm_params* p, int W, int H)
+{
+    SgbmEff e;
+    std::string why;
+    return resolve_sgbm(p, W, H, &e, &why);
+}
+
+int mvsv_bm_validate(const mvsv_bm_params* p, int W, int H)
+{
+    BmEff e;
+    std::string why;
+    return resolve_bm(p, W, H, &e, &why);
+}
+
+int mvsv_create(mvsv_ctx** out, int hip_device)
+{
+    if (!out) return MVSV_E_INVALID_ARG;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        (void)hipGetLastError();
+        return MVSV_E_NODEV;
+    }
+    if (hip_device < 0 || hip_device >= count) return MVSV_E_INVALID_ARG;
+    mvsv_ctx* c = new (std::nothrow) mvsv_ctx();
+    if (!c) return MVSV_E_OOM;
+    c->device = hip_device;
+    if (hipSetDevice(hip_device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        delete c;
+        return MVSV_E_HIP;
+    }
+    c->stream = c->own;
+    *out = c;
+    return MVSV_OK;
+}
+
+static void free_buf(DevBuf& b)
+{
+    if (b.ptr) (void)hipFree(b.ptr);
+    b.ptr = nullptr;
+    b.bytes = 0;
+}
+
+int mvsv_trim(mvsv_ctx* ctx)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    DevBuf* all[] = {&ctx->pre, &ctx->cost, &ctx->agg, &ctx->raw, &ctx->uf_parent, &ctx->uf_size,
+                     &ctx->bm_lf, &ctx->bm_rf, &ctx->bm_cost, &ctx->h_left, &ctx->h_right,
+                     &ctx->h_out};
+    for (DevBuf* b : all) free_buf(*b);
+    return MVSV_OK;
+}
+
+void mvsv_destroy(mvsv_ctx* ctx)
+{
+    if (!ctx) return;
+    mvsv_trim(ctx);
+    if (ctx->own) (void)hipStreamDestroy(ctx->own);
+    delete ctx;
+}
+
+const char* mvsv_last_error(const mvsv_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int mvsv_set_stream(mvsv_ctx* ctx, void* s)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    ctx->stream = s ? (hipStream_t)s : ctx->own;
+    return MVSV_OK;
+}
+
+void* mvsv_get_stream(mvsv_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int mvsv_synchronize(mvsv_ctx* ctx)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    (void)hipSetDevice(ctx->device);
+    return check_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+}
+
+size_t mvsv_sgbm_workspace_bytes(int n, int W, int H, const mvsv_sgbm_params* p)
+{
+    SgbmEff e;
+    std::string why;
+    if (n <= 0 || resolve_sgbm(p, W, H, &e, &why) != MVSV_OK) return 0;
+    size_t frame = (size_t)W * H;
+    size_t vol = e.W1 > 0 ? (size_t)e.W1 * H * e.D * 2 : 0;
+    size_t b = (size_t)n * (frame * 4 + 2 * vol + frame * 2);
+    if (e.speckle_window > 0) b += (size_t)n * frame * 8;
+    return b;
+}
+
+int mvsv_sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs,
+                     const uint8_t* R, size_t rs, size_t rfs, int W, int H,
+                     const mvsv_sgbm_params* p, int16_t* out, size_t os, size_t ofs)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    if (n <= 0 || !L || !R || !out) return set_error(ctx, MVSV_E_INVALID_ARG, "null buffer or n <= 0");
+    if (ls < (size_t)W || rs < (size_t)W || os < (size_t)W)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "stride smaller than width");
+    SgbmEff e;
+    std::string why;
+    int rc = resolve_sgbm(p, W, H, &e, &why);
+    if (rc) return set_error(ctx, rc, why);
+    (void)hipSetDevice(ctx->device);
+    return sgbm_device(ctx, n, L, ls, lfs, R, rs, rfs, W, H, e, out, os, ofs);
+}
+
+int mvsv_bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs,
+                   const uint8_t* R, size_t rs, size_t rfs, int W, int H,
+                   const mvsv_bm_params* p, int16_t* out, size_t os, size_t ofs)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    if (n <= 0 || !L || !R || !out) return set_error(ctx, MVSV_E_INVALID_ARG, "null buffer or n <= 0");
+    if (ls < (size_t)W || rs < (size_t)W || os < (size_t)W)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "stride smaller than width");
+    BmEff e;
+    std::string why;
+    int rc = resolve_bm(p, W, H, &e, &why);
+    if (rc) return set_error(ctx, rc, why);
+    (void)hipSetDevice(ctx->device);
+    return bm_device(ctx, n, L, ls, lfs, R, rs, rfs, W, H, e, out, os, ofs);
+}
+
+int mvsv_mean_disparity_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st,
+                                    size_t fs, int W, int H, float* means)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    if (n <= 0 || !dmap || !means || W <= 0 || H <= 0 || st < (size_t)W)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "bad mean-grid arguments");
+    (void)hipSetDevice(ctx->device);
+    return mean_grid_device(ctx, n, dmap, st, fs, W, H, means);
+}
+
+// Host-pointer path: stage through cached device buffers, run, copy back, sync.
+static int host_call(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* R, size_t rs,
+                     int W, int H, int16_t* out, size_t os, bool sgbm, const void* params)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    if (!L || !R || !out || W <= 0 || H <= 0)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "null buffer or empty image");
+    if (ls < (size_t)W || rs < (size_t)W || os < (size_t)W)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "stride smaller than width");
+    int rc;
+    SgbmEff se;
+    BmEff be;
+    std::string why;
+    rc = sgbm ? resolve_sgbm((const mvsv_sgbm_params*)params, W, H, &se, &why)
+              : resolve_bm((const mvsv_bm_params*)params, W, H, &be, &why);
+    if (rc) return set_error(ctx, rc, why);
+    (void)hipSetDevice(ctx->device);
+    size_t fb = (size_t)W * H;
+    if ((rc = ensure(ctx, ctx->h_left, fb, "left staging"))) return rc;
+    if ((rc = ensure(ctx, ctx->h_right, fb, "right staging"))) return rc;
+    if ((rc = ensure(ctx, ctx->h_out, fb * 2, "output staging"))) return rc;
+    hipStream_t s = ctx->stream;
+    if ((rc = check_hip(ctx, hipMemcpy2DAsync(ctx->h_left.ptr, W, L, ls, W, H, hipMemcpyHostToDevice, s), "H2D left"))) return rc;
+    if ((rc = check_hip(ctx, hipMemcpy2DAsync(ctx->h_right.ptr, W, R, rs, W, H, hipMemcpyHostToDevice, s), "H2D right"))) return rc;
+    int16_t* dout = (int16_t*)ctx->h_out.ptr;
+    rc = sgbm ? sgbm_device(ctx, 1, (const uint8_t*)ctx->h_left.ptr, W, fb,
+                            (const uint8_t*)ctx->h_right.ptr, W, fb, W, H, se, dout, W, fb)
+              : bm_device(ctx, 1, (const uint8_t*)ctx->h_left.ptr, W, fb,
+                          (const uint8_t*)ctx->h_right.ptr, W, fb, W, H, be, dout, W, fb);
+    if (rc) return rc;
+    if ((rc = check_hip(ctx, hipMemcpy2DAsync(out, os * 2, dout, (size_t)W * 2, (size_t)W * 2, H, hipMemcpyDeviceToHost, s), "D2H out"))) return rc;
+    return check_hip(ctx, hipStreamSynchronize(s), "hipStreamSynchronize");
+}
+
+int mvsv_sgbm(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* R, size_t rs, int W,
+              int H, const mvsv_sgbm_params* p, int16_t* out, size_t os)
+{
+    return host_call(ctx, L, ls, R, rs, W, H, out, os, true, p);
+}
+
+int mvsv_bm(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* R, size_t rs, int W,
+            int H, const mvsv_bm_params* p, int16_t* out, size_t os)
+{
+    return host_call(ctx, L, ls, R, rs, W, H, out, os, false, p);
+}
+
+// ---------------------------------------------------------------------------
+// Flat %YAML:1.0 "key: number" reader (the subset cv::FileStorage writes for
+// configs/sgbm.yml and configs/bm.yml). Numbers are rounded like cvRound.
+// ---------------------------------------------------------------------------
+static int read_flat_yaml(const char* path, std::map<std::string, double>* kv)
+{
+    if (!path) return MVSV_E_INVALID_ARG;
+    std::ifstream f(path);
+    if (!f.is_open()) return MVSV_E_IO;
+    std::string line;
+    bool first = true;
+    while (std::getline(f, line)) {
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        if (first) {
+            first = false;
+            if (line.rfind("%YAML", 0) == 0) continue;
+        }
+        size_t hash = line.find('#');
+        if (hash != std::string::npos) line = line.substr(0, hash);
+        if (line.find_first_not_of(" \t") == std::string::npos) continue;
+        if (line == "---" || line == "...") continue;
+        size_t colon = line.find(':');
+        if (colon == std::string::npos) continue;
+        std::string key = line.substr(0, colon);
+        std::string val = line.substr(colon + 1);
+        auto trim = [](std::string& s) {
+            size_t a = s.find_first_not_of(" \t\"'");
+            size_t b = s.find_last_not_of(" \t\"'");
+            s = a == std::string::npos ? std::string() : s.substr(a, b - a + 1);
+        };
+        trim(key);
+        trim(val);
+        if (key.empty() || val.empty()) continue;  // nested map / empty node
+        char* end = nullptr;
+        errno = 0;
+        double d = std::strtod(val.c_str(), &end);
+        if (end == val.c_str() || errno) continue;  // non-numeric: not an int node
+        (*kv)[key] = d;
+    }
+    return MVSV_OK;
+}
+
+static int kv_int(const std::map<std::string, double>& kv, const char* key, int dflt)
+{
+    auto it = kv.find(key);
+    return it == kv.end() ? dflt : (int)std::lrint(it->second);
+}
+
+int mvsv_load_sgbm_yaml(const char* path, mvsv_sgbm_params* p, mvsv_sgbm_yaml_values* v)
+{
+    std::map<std::string, double> kv;
+    int rc = read_flat_yaml(path, &kv);
+    if (rc) return rc;  // reference: LOG(ERROR) "Unable to open disparity parameters"
+    // src/disparity.cpp:67 — required nodes
+    for (const char* k : {"numDisp", "blockSize", "speckleWindowSize", "speckleWindowRange"})
+        if (!kv.count(k)) return MVSV_E_PARSE;
+    mvsv_sgbm_yaml_values tmp;
+    tmp.minDisp = kv_int(kv, "minDisp", 0);
+    tmp.numDisp = kv_int(kv, "numDisp", 0);
+    tmp.blockSize = kv_int(kv, "blockSize", 0);
+    tmp.disp12MaxDiff = kv_int(kv, "disp12MaxDiff", 0);
+    tmp.preFilterCap = kv_int(kv, "preFilterCap", 0);
+    tmp.uniquenessRatio = kv_int(kv, "uniquenessRatio", 0);
+    tmp.speckleWindowSize = kv_int(kv, "speckleWindowSize", 0);
+    tmp.speckleRange = kv_int(kv, "speckleWindowRange", 0);
+    tmp.disparityMode = kv_int(kv, "mode", 0);
+    if (v) *v = tmp;
+    if (p) {  // src/disparity.cpp:83-95 — eight setters + mode, P1/P2 untouched
+        p->min_disparity = tmp.minDisp;
+        p->num_disparities = tmp.numDisp;
+        p->block_size = tmp.blockSize;
+        p->pre_filter_cap = tmp.preFilterCap;
+        p->uniqueness_ratio = tmp.uniquenessRatio;
+        p->disp12_max_diff = tmp.disp12MaxDiff;
+        p->speckle_window_size = tmp.speckleWindowSize;
+        p->speckle_range = tmp.speckleRange;
+        p->mode = tmp.disparityMode == 1 ? MVSV_MODE_HH : MVSV_MODE_SGBM;
+    }
+    return MVSV_OK;
+}
+
+int mvsv_load_bm_yaml(const char* path, mvsv_bm_params* p)
+{
+    std::map<std::string, double> kv;
+    int rc = read_flat_yaml(path, &kv);
+    if (rc) return rc;
+    for (const char* k : {"numDisp", "blockSize"})
+        if (!kv.count(k)) return MVSV_E_PARSE;
+    if (p) {
+        p->num_disparities = kv_int(kv, "numDisp", p->num_disparities);
+        p->block_size = kv_int(kv, "blockSize", p->block_size);
+        p->pre_filter_cap = kv_int(kv, "preFilterCap", p->pre_filter_cap);
+        p->pre_filter_size = kv_int(kv, "preFilterSize", p->pre_filter_size);
+        p->uniqueness_ratio = kv_int(kv, "uniquenessRatio", p->uniqueness_ratio);
+        p->texture_threshold = kv_int(kv, "textureThreshold", p->texture_threshold);
+        p->min_disparity = kv_int(kv, "minDisp", p->min_disparity);
+        p->speckle_window_size = kv_int(kv, "speckleWindowSize", p->speckle_window_size);
+        p->speckle_range = kv_int(kv, "speckleWindowRange", p->speckle_range);
+        p->disp12_max_diff = kv_int(kv, "disp12MaxDiff", p->disp12_max_diff);
+        p->pre_filter_type = kv_int(kv, "preFilterType", p->pre_filter_type);
+    }
+    return MVSV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic rectified pair.
+// ---------------------------------------------------------------------------
+namespace {
+struct Pcg32 {
+    uint64_t state;
+    static constexpr uint64_t inc = 0xda3e39cb94b95bdbULL;
+    explicit Pcg32(uint32_t seed) : state((uint64_t)seed * 2u + 1u) {}
+    uint32_t next()
+    {
+        uint64_t old = state;
+        state = old * 6364136223846793005ULL + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((0u - rot) & 31u));
+    }
+};
+}  // namespace
+
+int mvsv_synth_pair(uint32_t seed, int W, int H, int minD, int D, uint8_t* Lout, uint8_t* Rout)
+{
+    if (W <= 0 || H <= 0 || D <= 0 || !Lout || !Rout) return MVSV_E_INVALID_ARG;
+    Pcg32 rng(seed);
+    size_t np = (size_t)W * H;
+    uint8_t* noise = (uint8_t*)std::malloc(np);
+    if (!noise) return MVSV_E_OOM;
+    for (size_t i = 0; i < np; i++) noise[i] = (uint8_t)(rng.next() >> 24);
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            int s = 0;
+            for (int dy = -1; dy <= 1; dy++)
+                for (int dx = -1; dx <= 1; dx++) {
+                    int yy = std::min(std::max(y + dy, 0), H - 1);
+                    int xx = std::min(std::max(x + dx, 0), W - 1);
+                    s += noise[(size_t)yy * W + xx];
+                }
+            Lout[(size_t)y * W + x] = (uint8_t)((2 * s + 9) / 18);  // round half up of s/9
+        }
+    std::free(noise);
+    const int rect = (int)std::floor(0.6 * D + 0.5);
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            bool in = x >= W / 3 && x < 2 * W / 3 && y >= H / 3 && y < 2 * H / 3;
+            int d = in ? rect : (int)std::floor(D / 8.0 + (D / 4.0) * y / H + 0.5);
+            d = std::min(std::max(d, minD), minD + D - 1);
+            int xs = std::min(std::max(x + d, 0), W - 1);
+            int v = Lout[(size_t)y * W + xs] + (int)(rng.next() % 3u) - 1;
+            Rout[(size_t)y * W + x] = (uint8_t)std::min(std::max(v, 0), 255);
+        }
+    return MVSV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,91 @@
+// mvsv_internal.hpp — shared declarations of libmvsv (host + HIP kernels).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+#include "../../include/mvsv.h"
+
+namespace mvsv {
+
+constexpr int kMaxCost = 32767;    // OpenCV StereoSGBM MAX_COST (SHRT_MAX)
+constexpr int kDispShift = 4;      // StereoMatcher::DISP_SHIFT
+constexpr int kDispScale = 16;
+
+// Effective StereoSGBM parameters after OpenCV's defaulting rules
+// ([OpenCV] computeDisparitySGBM prologue).
+struct SgbmEff {
+    int minD, maxD, D;
+    int SW2, SH2;
+    int ftzero;
+    int uniq, disp12;
+    int P1, P2;
+    int minX1, maxX1, W1;
+    int invalid;  // (minD - 1) * 16
+    int fullDP;   // MODE_HH
+    int variant;
+    int speckle_window, speckle_diff;  // speckle_diff = 16 * speckleRange
+};
+
+struct BmEff {
+    int ndisp, mindisp, wsz2, cap, tex, uniq;
+    int lofs, rofs, width1, ncol;
+    int xmin, xmax, ymin, ymax;  // validDisparityRect (half-open)
+    int filtered;                // (minD - 1) << 4
+    int disp12;                  // < 0: off
+    int speckle_window, speckle_range;
+    int prefilter_type, prefilter_size;
+};
+
+// Resolve + validate (OpenCV's asserts). Return MVSV_OK or MVSV_E_INVALID_ARG
+// and an explanation in *why.
+int resolve_sgbm(const mvsv_sgbm_params* p, int W, int H, SgbmEff* e, std::string* why);
+int resolve_bm(const mvsv_bm_params* p, int W, int H, BmEff* e, std::string* why);
+
+// Grow-only cached device buffer.
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace mvsv
+
+struct mvsv_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // SGBM
+    mvsv::DevBuf pre, cost, agg, raw, uf_parent, uf_size;
+    // BM
+    mvsv::DevBuf bm_lf, bm_rf, bm_cost;
+    // host-pointer staging
+    mvsv::DevBuf h_left, h_right, h_out;
+};
+
+namespace mvsv {
+
+int set_error(mvsv_ctx* ctx, int code, const std::string& msg);
+int ensure(mvsv_ctx* ctx, DevBuf& b, size_t bytes, const char* what);
+int check_hip(mvsv_ctx* ctx, hipError_t e, const char* what);
+
+// Device pipelines (defined in the .hip translation units). All enqueue on
+// ctx->stream. Strides are in elements.
+int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, const uint8_t* R,
+                size_t rs, size_t rfs, int W, int H, const SgbmEff& e, int16_t* out, size_t os,
+                size_t ofs);
+int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, const uint8_t* R,
+              size_t rs, size_t rfs, int W, int H, const BmEff& e, int16_t* out, size_t os,
+              size_t ofs);
+// Post filters shared by both matchers.
+int median3x3_device(mvsv_ctx* ctx, int n, const int16_t* src, size_t ss, size_t sfs,
+                     int16_t* dst, size_t ds, size_t dfs, int W, int H);
+int speckle_device(mvsv_ctx* ctx, int n, int16_t* img, size_t st, size_t fs, int W, int H,
+                   int new_val, int max_size, int max_diff);
+int mean_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_t fs, int W,
+                     int H, float* means);
+
+}  // namespace mvsv

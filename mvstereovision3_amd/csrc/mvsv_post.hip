@@ -1,0 +1,238 @@
+// mvsv_post.hip — post-filters of the disparity path on MI355X:
+//   * 3x3 median, replicate border  ([OpenCV] medianBlur(disp, disp, 3), applied
+//     by StereoSGBM::compute after the core)
+//   * speckle filter                ([OpenCV] filterSpeckles, CV_16S): 4-connected
+//     components of pixels != newVal whose neighbours differ by <= maxDiff;
+//     components of size <= maxSpeckleSize become newVal.  Computed with a
+//     lock-free union-find (atomicMin linking towards the smaller index), which
+//     yields exactly the same components as OpenCV's raster-order flood fill.
+//   * MeanDisparityDetection grid   (src/MeanDisparityDetection.cpp:159-206,
+//     Utility::calcMeanDisparity src/utility.cpp:265-285)
+#include "mvsv_device.hpp"
+#include "mvsv_internal.hpp"
+
+namespace mvsv {
+namespace {
+
+using namespace dev;
+
+__device__ __forceinline__ void sort2(int& a, int& b)
+{
+    int lo = min(a, b), hi = max(a, b);
+    a = lo;
+    b = hi;
+}
+
+// median of 9 with the 19-exchange network (Paeth / Devillard opt_med9)
+__device__ __forceinline__ int med9(int p0, int p1, int p2, int p3, int p4, int p5, int p6, int p7,
+                                    int p8)
+{
+    sort2(p1, p2); sort2(p4, p5); sort2(p7, p8);
+    sort2(p0, p1); sort2(p3, p4); sort2(p6, p7);
+    sort2(p1, p2); sort2(p4, p5); sort2(p7, p8);
+    sort2(p0, p3); sort2(p5, p8); sort2(p4, p7);
+    sort2(p3, p6); sort2(p1, p4); sort2(p2, p5);
+    sort2(p4, p7); sort2(p4, p2); sort2(p6, p4);
+    sort2(p4, p2);
+    return p4;
+}
+
+__global__ __launch_bounds__(256) void median3x3_kernel(const int16_t* __restrict__ src, size_t ss,
+                                                        size_t sfs, int16_t* __restrict__ dst,
+                                                        size_t ds, size_t dfs, int W, int H)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.z;
+    if (x >= W || y >= H) return;
+    const int16_t* s = src + f * sfs;
+    const int xm = max(x - 1, 0), xp = min(x + 1, W - 1);
+    const int16_t* r0 = s + (size_t)max(y - 1, 0) * ss;
+    const int16_t* r1 = s + (size_t)y * ss;
+    const int16_t* r2 = s + (size_t)min(y + 1, H - 1) * ss;
+    int m = med9(r0[xm], r0[x], r0[xp], r1[xm], r1[x], r1[xp], r2[xm], r2[x], r2[xp]);
+    dst[f * dfs + (size_t)y * ds + x] = (int16_t)m;
+}
+
+// ---- speckle filter: union-find ----------------------------------------------
+__device__ __forceinline__ int uf_load(const int* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ int uf_find(const int* parent, int i)
+{
+    int p = uf_load(parent + i);
+    while (p != i) {
+        i = p;
+        p = uf_load(parent + i);
+    }
+    return i;
+}
+
+__device__ void uf_unite(int* parent, int a, int b)
+{
+    for (;;) {
+        a = uf_find(parent, a);
+        b = uf_find(parent, b);
+        if (a == b) return;
+        if (a > b) {
+            int t = a;
+            a = b;
+            b = t;
+        }
+        int old = atomicMin(parent + b, a);  // link root b under a (a < b)
+        if (old == b) return;
+        b = old;  // b was re-linked concurrently: retry from its new parent
+    }
+}
+
+__global__ __launch_bounds__(256) void speckle_init_kernel(int* __restrict__ parent,
+                                                           int* __restrict__ size, int npix)
+{
+    const int f = blockIdx.y;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < npix; i += gridDim.x * 256) {
+        parent[(size_t)f * npix + i] = i;
+        size[(size_t)f * npix + i] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void speckle_merge_kernel(const int16_t* __restrict__ img,
+                                                            size_t st, size_t fs, int W, int H,
+                                                            int new_val, int max_diff,
+                                                            int* __restrict__ parent)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.z;
+    if (x >= W || y >= H) return;
+    const int16_t* s = img + f * fs;
+    int* par = parent + (size_t)f * W * H;
+    const int v = s[(size_t)y * st + x];
+    if (v == new_val) return;
+    const int i = y * W + x;
+    if (x + 1 < W) {
+        int u = s[(size_t)y * st + x + 1];
+        if (u != new_val && abs(v - u) <= max_diff) uf_unite(par, i, i + 1);
+    }
+    if (y + 1 < H) {
+        int u = s[(size_t)(y + 1) * st + x];
+        if (u != new_val && abs(v - u) <= max_diff) uf_unite(par, i, i + W);
+    }
+}
+
+__global__ __launch_bounds__(256) void speckle_count_kernel(const int16_t* __restrict__ img,
+                                                            size_t st, size_t fs, int W, int H,
+                                                            int new_val, int* __restrict__ parent,
+                                                            int* __restrict__ size)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.z;
+    if (x >= W || y >= H) return;
+    const int v = img[f * fs + (size_t)y * st + x];
+    if (v == new_val) return;
+    int* par = parent + (size_t)f * W * H;
+    const int i = y * W + x;
+    const int r = uf_find(par, i);
+    par[i] = r;  // compression: only ever points at the root
+    atomicAdd(size + (size_t)f * W * H + r, 1);
+}
+
+__global__ __launch_bounds__(256) void speckle_apply_kernel(int16_t* __restrict__ img, size_t st,
+                                                            size_t fs, int W, int H, int new_val,
+                                                            int max_size,
+                                                            const int* __restrict__ parent,
+                                                            const int* __restrict__ size)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.z;
+    if (x >= W || y >= H) return;
+    int16_t* p = img + f * fs + (size_t)y * st + x;
+    if (*p == new_val) return;
+    const size_t base = (size_t)f * W * H;
+    const int r = parent[base + y * W + x];
+    if (size[base + r] <= max_size) *p = (int16_t)new_val;
+}
+
+// ---- MeanDisparityDetection::build(MEAN_VALUE) --------------------------------
+__global__ __launch_bounds__(256) void mean_grid_kernel(const int16_t* __restrict__ dmap,
+                                                        size_t st, size_t fs, int W, int H,
+                                                        float* __restrict__ means)
+{
+    __shared__ int s_tot[4], s_cnt[4];
+    const int tile = blockIdx.x;  // 0..80, row-major 9x9
+    const int f = blockIdx.y;
+    const int r = tile / 9, c = tile % 9;
+    const int dx = W / 9, dy = H / 9;
+    const int16_t* m = dmap + f * fs;
+    int tot = 0, cnt = 0;
+    for (int i = threadIdx.x; i < dx * dy; i += 256) {
+        int yy = r * dy + i / dx, xx = c * dx + i % dx;
+        int v = m[(size_t)yy * st + xx];
+        if (v > 1) {
+            tot += v;
+            cnt++;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        tot += __shfl_xor(tot, o);
+        cnt += __shfl_xor(cnt, o);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_tot[w] = tot;
+        s_cnt[w] = cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int T = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
+        int N = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        means[(size_t)f * 81 + tile] = (T == 0 || N == 0) ? 0.0f : (float)(T / abs(N));
+    }
+}
+
+}  // namespace
+
+int median3x3_device(mvsv_ctx* ctx, int n, const int16_t* src, size_t ss, size_t sfs, int16_t* dst,
+                     size_t ds, size_t dfs, int W, int H)
+{
+    dim3 grid((W + 63) / 64, (H + 3) / 4, n);
+    hipLaunchKernelGGL(median3x3_kernel, grid, dim3(256), 0, ctx->stream, src, ss, sfs, dst, ds,
+                       dfs, W, H);
+    return check_hip(ctx, hipGetLastError(), "median3x3");
+}
+
+int speckle_device(mvsv_ctx* ctx, int n, int16_t* img, size_t st, size_t fs, int W, int H,
+                   int new_val, int max_size, int max_diff)
+{
+    int rc;
+    const size_t npix = (size_t)W * H;
+    if ((rc = ensure(ctx, ctx->uf_parent, (size_t)n * npix * 4, "speckle labels"))) return rc;
+    if ((rc = ensure(ctx, ctx->uf_size, (size_t)n * npix * 4, "speckle sizes"))) return rc;
+    int* parent = (int*)ctx->uf_parent.ptr;
+    int* size = (int*)ctx->uf_size.ptr;
+    hipStream_t s = ctx->stream;
+    int blocks = (int)std::min<size_t>((npix + 255) / 256, 2048);
+    hipLaunchKernelGGL(speckle_init_kernel, dim3(blocks, n), dim3(256), 0, s, parent, size,
+                       (int)npix);
+    dim3 grid((W + 63) / 64, (H + 3) / 4, n);
+    hipLaunchKernelGGL(speckle_merge_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val,
+                       max_diff, parent);
+    hipLaunchKernelGGL(speckle_count_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val,
+                       parent, size);
+    hipLaunchKernelGGL(speckle_apply_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val,
+                       max_size, parent, size);
+    return check_hip(ctx, hipGetLastError(), "speckle filter");
+}
+
+int mean_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_t fs, int W, int H,
+                     float* means)
+{
+    hipLaunchKernelGGL(mean_grid_kernel, dim3(81, n), dim3(256), 0, ctx->stream, dmap, st, fs, W,
+                       H, means);
+    return check_hip(ctx, hipGetLastError(), "mean disparity grid");
+}
+
+}  // namespace mvsv

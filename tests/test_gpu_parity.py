@@ -1,0 +1,247 @@
+"""HIP path vs the CPU oracle, bit-exact (int16 disparity x 16).
+
+Every test calls the kernels through the C ABI (libmvsv.so via the host mirror
+in mvstereovision3_amd.disparity) and compares with oracle/ (OpenCV 3.4
+restatement; parity unpinned, see oracle/mvsv_oracle.h).  Sizes: random small
+cases in the seconds range for the oracle, plus the BASELINE.json configs at
+full size (640x480 and 1280x960).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED0 = 0x5EED0000
+
+
+def report(a, b):
+    bad = np.argwhere(a != b)
+    if bad.size == 0:
+        return ""
+    pts = [(int(y), int(x), int(a[y, x]), int(b[y, x])) for y, x in bad[:10]]
+    return f"{len(bad)} mismatches of {a.size}; first (y, x, gpu, oracle): {pts}"
+
+
+def sgbm_both(mvsv, oracle, L, R, variant=0, **kw):
+    names = dict(minDisparity="min_disparity", numDisparities="num_disparities",
+                 blockSize="block_size", P1="p1", P2="p2", disp12MaxDiff="disp12_max_diff",
+                 preFilterCap="pre_filter_cap", uniquenessRatio="uniqueness_ratio",
+                 speckleWindowSize="speckle_window_size", speckleRange="speckle_range", mode="mode")
+    m = mvsv.StereoSGBM.create(**kw)
+    m.setVariant(variant)
+    got = m.compute(L, R)
+    p = {v: int(kw.get(k, d)) for (k, v), d in zip(names.items(),
+                                                    (0, 16, 3, 0, 0, 0, 0, 0, 0, 0, 0))}
+    want = oracle.sgbm(L, R, p, flags=variant)
+    return got, want
+
+
+def bm_both(mvsv, oracle, L, R, p):
+    m = mvsv.StereoBM.create(p["num_disparities"], p["block_size"])
+    m._params.pre_filter_type = p["pre_filter_type"]
+    m._params.pre_filter_size = p["pre_filter_size"]
+    m._params.pre_filter_cap = p["pre_filter_cap"]
+    m._params.min_disparity = p["min_disparity"]
+    m._params.texture_threshold = p["texture_threshold"]
+    m._params.uniqueness_ratio = p["uniqueness_ratio"]
+    m._params.speckle_window_size = p["speckle_window_size"]
+    m._params.speckle_range = p["speckle_range"]
+    m._params.disp12_max_diff = p["disp12_max_diff"]
+    return m.compute(L, R), oracle.bm(L, R, p)
+
+
+def rand_pair(rng, H, W, shift, kind):
+    if kind == 0:
+        from scipy.ndimage import uniform_filter
+        L = uniform_filter(rng.integers(0, 256, (H, W)).astype(float), 3).round().astype(np.uint8)
+    elif kind == 1:  # low texture: ties, texture filter, saturation
+        L = (rng.integers(0, 4, (H, W)) * 60).astype(np.uint8)
+        L[:, W // 3:W // 2] = 128
+    else:
+        L = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    R = np.roll(L, -shift, axis=1)
+    R = np.clip(R.astype(int) + rng.integers(-2, 3, R.shape), 0, 255).astype(np.uint8)
+    return L, R
+
+
+# ---------------------------------------------------------------- SGBM -----
+@pytest.mark.parametrize("seed", range(24))
+def test_sgbm_random_small(gpu, mvsv, oracle, seed):
+    rng = np.random.default_rng(1000 + seed)
+    H, W = int(rng.integers(12, 70)), int(rng.integers(48, 120))
+    D = int(rng.choice([16, 32, 48, 64]))
+    kw = dict(minDisparity=int(rng.integers(-6, 6)), numDisparities=D,
+              blockSize=int(rng.choice([0, 1, 3, 5, 7, 9, 11])),
+              P1=int(rng.choice([0, 2, 72, 300])), P2=int(rng.choice([0, 5, 288, 2000, 4000])),
+              disp12MaxDiff=int(rng.integers(-1, 4)),
+              preFilterCap=int(rng.choice([0, 15, 31, 63])),
+              uniquenessRatio=int(rng.choice([-1, 0, 5, 15])),
+              speckleWindowSize=int(rng.choice([0, 10, 50])),
+              speckleRange=int(rng.choice([1, 2, 4])), mode=int(rng.integers(0, 2)))
+    if W + min(kw["minDisparity"], 0) - max(kw["minDisparity"] + D, 0) <= max(kw["blockSize"], 5) // 2:
+        kw["numDisparities"] = 16
+    L, R = rand_pair(rng, H, W, int(rng.integers(0, 16)), int(rng.integers(0, 3)))
+    variant = int(rng.integers(0, 4))
+    got, want = sgbm_both(mvsv, oracle, L, R, variant=variant, **kw)
+    assert np.array_equal(got, want), f"{kw} variant={variant}: " + report(got, want)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("D", [16, 128, 256])
+def test_sgbm_synthetic_modes(gpu, mvsv, oracle, mode, D):
+    L, R = mvsv.synth_pair(SEED0 + D, 320, 96, 0, D) if D < 256 else \
+        mvsv.synth_pair(SEED0 + D, 400, 64, 0, D)
+    got, want = sgbm_both(mvsv, oracle, L, R, minDisparity=0, numDisparities=D, blockSize=9,
+                          P1=8 * 81, P2=32 * 81, uniquenessRatio=5, speckleWindowSize=40,
+                          speckleRange=2, mode=mode)
+    assert np.array_equal(got, want), report(got, want)
+
+
+def test_sgbm_all_invalid_when_no_columns(gpu, mvsv, oracle):
+    L, R = mvsv.synth_pair(SEED0, 40, 20, 0, 64)
+    got, want = sgbm_both(mvsv, oracle, L, R, minDisparity=0, numDisparities=64, blockSize=5)
+    assert np.array_equal(got, want)
+    assert (got == -16).all()
+
+
+def test_sgbm_roi_views(gpu, mvsv, oracle):
+    """Stereopair images are cropped cv::Mat views (stride != width)."""
+    big_L, big_R = mvsv.synth_pair(SEED0 + 7, 300, 120, 0, 64)
+    L, R = big_L[10:100, 20:260], big_R[10:100, 20:260]
+    assert L.strides[0] == 300
+    got, want = sgbm_both(mvsv, oracle, L, R, minDisparity=0, numDisparities=64, blockSize=7)
+    assert np.array_equal(got, want), report(got, want)
+
+
+def test_sgbm_reference_call_sites(gpu, mvsv, oracle):
+    """liveDisparity create(0,64,9,8*81,32*81) and captureDisparity create(0,16,5,200,800)."""
+    L, R = mvsv.synth_pair(SEED0 + 3, 376, 240, 0, 64)  # 2x2-binned mvBlueFOX size
+    for kw in (dict(minDisparity=0, numDisparities=64, blockSize=9, P1=648, P2=2592),
+               dict(minDisparity=0, numDisparities=16, blockSize=5, P1=200, P2=800)):
+        got, want = sgbm_both(mvsv, oracle, L, R, **kw)
+        assert np.array_equal(got, want), f"{kw}: " + report(got, want)
+
+
+def test_sgbm_loader_config(gpu, mvsv, oracle):
+    """configs/sgbm.yml through Disparity::loadSGBMParameters + Disparity::sgbm."""
+    import os
+    from tests.conftest import CONFIGS
+    m = mvsv.StereoSGBM.create(0, 0, 0, 8 * 0 * 0, 32 * 0 * 0)  # trgt/mean_test.cpp:233-237
+    para = mvsv.sgbmParameters()
+    assert mvsv.Disparity.loadSGBMParameters(os.path.join(CONFIGS, "sgbm.yml"), m, para)
+    L, R = mvsv.synth_pair(SEED0 + 11, 320, 120, 1, 128)
+    out = mvsv.Disparity.sgbm(mvsv.Stereopair(L, R), None, m)
+    p = dict(m.params())
+    p.pop("variant")
+    want = oracle.sgbm(L, R, p)
+    assert np.array_equal(out, want), report(out, want)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("mode", [0, 1])
+def test_sgbm_config3_640x480(gpu, mvsv, oracle, mode):
+    """BASELINE config 3: configs/sgbm.yml, 640x480, 128 disparities (mode 0 and 8-path)."""
+    L, R = mvsv.synth_pair(SEED0, 640, 480, 1, 128)
+    got, want = sgbm_both(mvsv, oracle, L, R, minDisparity=1, numDisparities=128, blockSize=13,
+                          disp12MaxDiff=0, preFilterCap=0, uniquenessRatio=0,
+                          speckleWindowSize=150, speckleRange=2, mode=mode)
+    assert np.array_equal(got, want), report(got, want)
+
+
+@pytest.mark.slow
+def test_sgbm_config4_1280x960_hh(gpu, mvsv, oracle):
+    """Headline workload frame: 1280x960, D=128, 8 paths (sgbm.yml values, mode 1)."""
+    L, R = mvsv.synth_pair(SEED0 + 1, 1280, 960, 1, 128)
+    got, want = sgbm_both(mvsv, oracle, L, R, minDisparity=1, numDisparities=128, blockSize=13,
+                          speckleWindowSize=150, speckleRange=2, mode=1)
+    assert np.array_equal(got, want), report(got, want)
+
+
+def test_sgbm_device_batch(gpu, mvsv, oracle):
+    """Frame batch on HBM-resident torch tensors == per-frame oracle."""
+    torch = gpu
+    frames = [mvsv.synth_pair(SEED0 + i, 256, 128, 0, 64) for i in range(3)]
+    Lt = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
+    Rt = torch.from_numpy(np.stack([f[1] for f in frames])).cuda()
+    m = mvsv.StereoSGBM.create(0, 64, 7, 8 * 49, 32 * 49, 1, 31, 10, 30, 2, mvsv.MODE_HH)
+    out = m.compute(Lt, Rt)
+    torch.cuda.synchronize()
+    out = out.cpu().numpy()
+    p = dict(m.params())
+    p.pop("variant")
+    for i, (L, R) in enumerate(frames):
+        want = oracle.sgbm(L, R, p)
+        assert np.array_equal(out[i], want), f"frame {i}: " + report(out[i], want)
+
+
+# ------------------------------------------------------------------ BM -----
+@pytest.mark.parametrize("seed", range(16))
+def test_bm_random_small(gpu, mvsv, oracle, seed):
+    rng = np.random.default_rng(2000 + seed)
+    H, W = int(rng.integers(24, 80)), int(rng.integers(60, 140))
+    bs = int(rng.choice([5, 7, 9, 11, 21]))
+    if bs >= min(H, W):
+        bs = 5
+    p = dict(pre_filter_type=1, pre_filter_size=9, pre_filter_cap=int(rng.integers(1, 64)),
+             block_size=bs, min_disparity=int(rng.integers(-4, 4)),
+             num_disparities=int(rng.choice([16, 32])),
+             texture_threshold=int(rng.choice([0, 10, 100])),
+             uniqueness_ratio=int(rng.choice([0, 10, 15])),
+             speckle_window_size=int(rng.choice([0, 10])),
+             speckle_range=int(rng.choice([0, 4, 32])),
+             disp12_max_diff=int(rng.choice([-1, 0, 1, 3])))
+    L, R = rand_pair(rng, H, W, int(rng.integers(0, 16)), int(rng.integers(0, 3)))
+    got, want = bm_both(mvsv, oracle, L, R, p)
+    assert np.array_equal(got, want), f"{p}: " + report(got, want)
+
+
+def bm_defaults(D, bs):
+    return dict(pre_filter_type=1, pre_filter_size=9, pre_filter_cap=31, block_size=bs,
+                min_disparity=0, num_disparities=D, texture_threshold=10, uniqueness_ratio=15,
+                speckle_window_size=0, speckle_range=0, disp12_max_diff=-1)
+
+
+def test_bm_config1_bm_yml(gpu, mvsv, oracle):
+    """BASELINE config 1: configs/bm.yml on a 640x480 pair."""
+    import os
+    from tests.conftest import CONFIGS
+    m = mvsv.StereoBM.create(16, 9)
+    assert mvsv.Disparity.loadBMParameters(os.path.join(CONFIGS, "bm.yml"), m)
+    L, R = mvsv.synth_pair(SEED0 + 21, 640, 480, 0, 80)
+    got = mvsv.Disparity.bm(mvsv.Stereopair(L, R), None, m)
+    want = oracle.bm(L, R, m.params())
+    assert np.array_equal(got, want), report(got, want)
+
+
+def test_bm_config2_640x480(gpu, mvsv, oracle):
+    """BASELINE config 2: StereoBM::create(64, 9) defaults, 640x480."""
+    L, R = mvsv.synth_pair(SEED0 + 22, 640, 480, 0, 64)
+    got, want = bm_both(mvsv, oracle, L, R, bm_defaults(64, 9))
+    assert np.array_equal(got, want), report(got, want)
+
+
+def test_bm_validate_and_speckle(gpu, mvsv, oracle):
+    L, R = mvsv.synth_pair(SEED0 + 23, 320, 200, 0, 48)
+    p = bm_defaults(48, 11)
+    p.update(disp12_max_diff=1, speckle_window_size=60, speckle_range=16, uniqueness_ratio=5)
+    got, want = bm_both(mvsv, oracle, L, R, p)
+    assert np.array_equal(got, want), report(got, want)
+
+
+# ---------------------------------------------------------- post-pass ------
+def test_mean_disparity_grid(gpu, mvsv, oracle):
+    torch = gpu
+    L, R = mvsv.synth_pair(SEED0 + 5, 640, 240, 0, 64)
+    d = mvsv.StereoSGBM.create(0, 64, 9, 648, 2592).compute(L, R)
+    work = d[:, 32:]  # createDMapROIS: x in [numDisp/2, cols)
+    got = mvsv.mean_disparity_grid(torch.from_numpy(np.ascontiguousarray(work)).cuda()).cpu().numpy()
+    want = oracle.mean_disparity_grid(work)
+    assert np.array_equal(got, want)
+
+
+def test_invalid_params_raise(gpu, mvsv):
+    L, R = mvsv.synth_pair(SEED0, 64, 48, 0, 16)
+    with pytest.raises(mvsv.MvsvError):
+        mvsv.StereoSGBM.create(0, 24, 5).compute(L, R)  # numDisparities % 16 != 0
+    with pytest.raises(mvsv.MvsvError):
+        mvsv.StereoBM.create(16, 4).compute(L, R)  # even block size
