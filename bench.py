@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X stereo disparity engine.
+
+Metric (BASELINE.json): "Mpix disparities/sec (SGBM 128-disp, 8-path) at
+1/2/4/8 GPUs; % HBM roofline".  Workload = BASELINE config 4, the largest
+single-GPU configuration of the metric: StereoSGBM on 1280x960 synthetic
+rectified pairs, configs/sgbm.yml values (minDisparity 1, 128 disparities,
+blockSize 13, P1/P2 = OpenCV defaults 2/5, speckle 150/2) with mode forced to
+MODE_HH (8 paths), a batch of 8 frames per GPU (config 4 = 64 frames over 8
+GPUs; weak scaling: per-GPU work fixed).
+
+One step = one batch of frames through the full StereoSGBM::compute path
+(prefilter, cost volume, 8 path aggregations, WTA/uniqueness/sub-pixel/LR,
+median, speckle) with inputs already resident in HBM, plus -- for N > 1 -- the
+RCCL gather of the int16 maps to rank 0 (the only exchange step of the
+frame-parallel batch mode).
+
+Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch with
+python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+SEED0 = 0x5EED0000
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SGBM_YML = os.path.join(ROOT, "tests", "golden", "configs", "sgbm.yml")
+PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=8, help="frames per GPU per step")
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=960)
+    ap.add_argument("--mode", type=int, default=1, help="1 = MODE_HH (8 paths), 0 = 5 paths")
+    ap.add_argument("--cpu-frames", type=int, default=8)
+    ap.add_argument("--cpu-threads", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    return ap.parse_args()
+
+
+def stage_bytes(stage, F, W, H, W1, D, ndir):
+    """Algorithmic HBM bytes of one step per stage ("Kernels")."""
+    vol2 = W1 * H * D * 2
+    px = W * H
+    return {
+        "prefilter": F * (2 * px + 4 * px),
+        "cost_volume": F * (4 * px + vol2),
+        "cost_fixup": 0,
+        # first direction writes S from C, the others read C, read S, write S
+        "path_aggregation": F * vol2 * (2 + 3 * (ndir - 1)),
+        "final_wta_lr": F * (2 * vol2 + 2 * px),
+        "post_filters": F * 4 * px,
+    }.get(stage, 0)
+
+
+def cpu_baseline(frames, params, threads):
+    """Oracle (scalar C restatement of OpenCV 3.4, 'port') on host cores, one frame per thread."""
+    from oracle import pyoracle
+    pyoracle.lib()
+    p = {k: v for k, v in params.items() if k != "variant"}
+    outs = [None] * len(frames)
+    nxt = [0]
+    lock = threading.Lock()
+
+    def worker():
+        while True:
+            with lock:
+                i = nxt[0]
+                nxt[0] += 1
+            if i >= len(frames):
+                return
+            L, R = frames[i]
+            outs[i] = pyoracle.sgbm(L, R, p)  # ctypes releases the GIL
+
+    t0 = time.perf_counter()
+    ts = [threading.Thread(target=worker) for _ in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return time.perf_counter() - t0, outs
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import mvstereovision3_amd as mvsv
+    from mvstereovision3_amd import _lib
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    W, H, F = args.width, args.height, args.frames
+    m = mvsv.StereoSGBM.create(0, 0, 0, 8 * 0 * 0, 32 * 0 * 0)  # trgt/mean_test.cpp:233-237
+    para = mvsv.sgbmParameters()
+    assert mvsv.Disparity.loadSGBMParameters(SGBM_YML, m, para), "cannot load sgbm.yml"
+    m.setMode(args.mode)
+    params = m.params()
+    D, minD = params["num_disparities"], params["min_disparity"]
+    W1 = W - max(minD + D, 0) + min(minD, 0)
+    ndir = 8 if args.mode == 1 else 5
+
+    host = [mvsv.synth_pair(SEED0 + rank * F + j, W, H, minD, D) for j in range(F)]
+    Lt = torch.from_numpy(np.stack([h[0] for h in host])).to(dev)
+    Rt = torch.from_numpy(np.stack([h[1] for h in host])).to(dev)
+    out = torch.empty((F, H, W), dtype=torch.int16, device=dev)
+    gather = world > 1 and not args.no_gather
+    gathered = [torch.empty_like(out) for _ in range(world)] if (gather and rank == 0) else None
+
+    def step():
+        m.compute(Lt, Rt, out)
+        if gather:
+            dist.gather(out, gathered if rank == 0 else None, dst=0)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier(device_ids=[local])
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        step()
+    ctx = _lib.context(local)
+    barrier()
+    _lib.profile_reset(ctx)
+    _lib.profile_enable(ctx, True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    t1 = time.perf_counter()
+    _lib.profile_enable(ctx, False)
+    prof = _lib.profile_read(ctx)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        K = args.steps
+        ms_per_step = elapsed / K * 1e3
+        mpix = world * F * W * H * K / elapsed / 1e6
+        stages = {k: {"ms_per_step": v[0] / K, "launches_per_step": v[1] / K}
+                  for k, v in prof.items() if v[1]}
+        dom = max(stages, key=lambda k: stages[k]["ms_per_step"])
+        launches = stages[dom]["launches_per_step"]
+        bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir) / launches
+        avg_launch_s = stages[dom]["ms_per_step"] / launches / 1e3
+        achieved = bytes_per_launch / avg_launch_s / 1e9
+        traffic = None
+        if os.path.exists(PMC_FILE):
+            try:
+                pmc = json.load(open(PMC_FILE))
+                if pmc.get("workload") == f"sgbm_{W}x{H}_d{D}_{ndir}path_batch{F}":
+                    traffic = pmc.get("stages", {}).get(dom, {}).get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        comp = 4 * W * H * (1 + D)  # SURVEY.md §8(d) compulsory bytes per frame, 8 paths
+        res = {
+            "metric": "Mpix disparities/sec (SGBM 128-disp, 8-path) at 1/2/4/8 GPUs; % HBM roofline",
+            "value": round(mpix, 2),
+            "unit": "Mpix/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int16",
+            "data": "synthetic (PCG32 rectified pairs, SURVEY.md §8(d)), HBM-resident",
+            "config": {"workload": f"sgbm_{W}x{H}_d{D}_{ndir}path_batch{F}",
+                       "width": W, "height": H, "num_disparities": D, "min_disparity": minD,
+                       "block_size": params["block_size"], "mode": "MODE_HH" if args.mode == 1 else "MODE_SGBM",
+                       "paths": ndir, "frames_per_gpu": F, "global_batch": F * world,
+                       "params": "configs/sgbm.yml + mode", "gather": "rccl" if gather else "none",
+                       "parallelism": f"frame-parallel x{world}"},
+            "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                         "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
+            "pipeline_compulsory": {"bytes_per_frame": comp,
+                                    "achieved_GBps_per_gpu": round(comp * F * K / elapsed / 1e9, 1),
+                                    "frac_of_peak": round(comp * F * K / elapsed / 1e9 / HBM_PEAK_GBPS, 5)},
+            "stages_ms_per_step": {k: round(v["ms_per_step"], 4) for k, v in stages.items()},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            nf = min(args.cpu_frames, F)
+            thr = max(1, min(args.cpu_threads, nf))
+            wall, ref = cpu_baseline(host[:nf], params, thr)
+            gpu_out = out[:nf].cpu().numpy()
+            same = sum(int(np.array_equal(gpu_out[i], ref[i])) for i in range(nf))
+            res["cpu_baseline"] = {"value": round(nf * W * H / wall / 1e6, 3), "unit": "Mpix/s",
+                                   "cores": thr, "kind": "port",
+                                   "sample": f"{nf} frames of the same workload, one frame per "
+                                             f"thread, scalar C oracle (OpenCV 3.4 restatement, "
+                                             f"no SIMD), {wall:.1f} s wall"}
+            res["parity_sample"] = f"{same}/{nf} frames bit-exact vs oracle"
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

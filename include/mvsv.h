@@ -190,6 +190,17 @@ MVSV_API int mvsv_load_sgbm_yaml(const char* path, mvsv_sgbm_params* p,
  * required. */
 MVSV_API int mvsv_load_bm_yaml(const char* path, mvsv_bm_params* p);
 
+/* Stage profiling with HIP events recorded on the context stream (used by
+ * bench.py to time the dominant kernel live).  Stages: 0 prefilter, 1 cost
+ * volume, 2 cost fixup, 3 path aggregation (one launch per direction),
+ * 4 final direction + WTA/LR, 5 post-filters (median + speckle), 6 BM match. */
+#define MVSV_NUM_STAGES 7
+MVSV_API int mvsv_profile_enable(mvsv_ctx* ctx, int on);
+MVSV_API int mvsv_profile_reset(mvsv_ctx* ctx);
+/* Synchronizes, then writes accumulated milliseconds and launch counts per stage. */
+MVSV_API int mvsv_profile_read(mvsv_ctx* ctx, double* stage_ms, int* stage_launches, int n);
+MVSV_API const char* mvsv_profile_stage_name(int stage);
+
 /* Deterministic synthetic rectified pair: PCG32 noise,
  * 3x3 box blur, slanted-plane + rectangle disparity field, +-1 noise.
  * Host buffers of width*height bytes each. */

@@ -30,6 +30,8 @@ PREFILTER_XSOBEL = 1
 VARIANT_FIRSTCOL_FIX = 1
 VARIANT_WTA_MIN_D = 2
 
+NUM_STAGES = 7
+
 _CODES = {
     MVSV_E_INVALID_ARG: "invalid argument",
     MVSV_E_HIP: "HIP error",
@@ -107,6 +109,10 @@ def _declare(lib):
         "mvsv_load_sgbm_yaml": ([ctypes.c_char_p, P, P], I),
         "mvsv_load_bm_yaml": ([ctypes.c_char_p, P], I),
         "mvsv_synth_pair": ([ctypes.c_uint32, I, I, I, I, P, P], I),
+        "mvsv_profile_enable": ([P, I], I),
+        "mvsv_profile_reset": ([P], I),
+        "mvsv_profile_read": ([P, P, P, I], I),
+        "mvsv_profile_stage_name": ([I], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -175,3 +181,19 @@ def context(device: int = 0) -> Context:
     if c is None:
         c = ctxs[device] = Context(device)
     return c
+
+
+def profile_enable(ctx: Context, on: bool = True):
+    check(lib().mvsv_profile_enable(ctx.handle, 1 if on else 0), ctx.handle)
+
+
+def profile_reset(ctx: Context):
+    check(lib().mvsv_profile_reset(ctx.handle), ctx.handle)
+
+
+def profile_read(ctx: Context) -> dict:
+    """{stage_name: (total_ms, launches)} accumulated since the last reset."""
+    ms = (ctypes.c_double * NUM_STAGES)()
+    n = (ctypes.c_int * NUM_STAGES)()
+    check(lib().mvsv_profile_read(ctx.handle, ms, n, NUM_STAGES), ctx.handle)
+    return {lib().mvsv_profile_stage_name(i).decode(): (ms[i], n[i]) for i in range(NUM_STAGES)}

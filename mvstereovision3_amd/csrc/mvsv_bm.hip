@@ -299,6 +299,7 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
                             "bm LDS attribute")))
             return rc;
     }
+    StageTimer tm(ctx, kStageBm);
     if (small)
         hipLaunchKernelGGL(bm_match_kernel<uint16_t>, grid, dim3(256), lay.bytes, s, Lf, Rf, W, H,
                            e, validate ? 1 : 0, out, os, ofs, cost);

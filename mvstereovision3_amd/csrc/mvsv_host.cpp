@@ -52,6 +52,36 @@ int ensure(mvsv_ctx* ctx, DevBuf& b, size_t bytes, const char* what)
     return MVSV_OK;
 }
 
+static hipEvent_t pool_get(mvsv_ctx* ctx)
+{
+    if (!ctx->event_pool.empty()) {
+        hipEvent_t e = ctx->event_pool.back();
+        ctx->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return e;
+}
+
+StageTimer::StageTimer(mvsv_ctx* c, int s) : ctx(c), stage(s)
+{
+    if (!ctx->prof) return;
+    a = pool_get(ctx);
+    b = pool_get(ctx);
+    if (a) (void)hipEventRecord(a, ctx->stream);
+}
+
+StageTimer::~StageTimer()
+{
+    if (!ctx->prof || !a || !b) return;
+    (void)hipEventRecord(b, ctx->stream);
+    ctx->marks.push_back({stage, a, b});
+}
+
 // [OpenCV] StereoSGBMImpl::compute asserts + computeDisparitySGBM prologue.
 int resolve_sgbm(const mvsv_sgbm_params* p, int W, int H, SgbmEff* e, std::string* why)
 {
@@ -250,10 +280,63 @@ int mvsv_trim(mvsv_ctx* ctx)
     return MVSV_OK;
 }
 
+static const char* kStageNames[MVSV_NUM_STAGES] = {
+    "prefilter", "cost_volume", "cost_fixup", "path_aggregation", "final_wta_lr", "post_filters",
+    "bm_match"};
+
+const char* mvsv_profile_stage_name(int s)
+{
+    return (s >= 0 && s < MVSV_NUM_STAGES) ? kStageNames[s] : "";
+}
+
+int mvsv_profile_enable(mvsv_ctx* ctx, int on)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    ctx->prof = on ? 1 : 0;
+    return MVSV_OK;
+}
+
+int mvsv_profile_reset(mvsv_ctx* ctx)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& m : ctx->marks) {
+        ctx->event_pool.push_back(m.a);
+        ctx->event_pool.push_back(m.b);
+    }
+    ctx->marks.clear();
+    return MVSV_OK;
+}
+
+int mvsv_profile_read(mvsv_ctx* ctx, double* ms, int* launches, int n)
+{
+    if (!ctx || n < 0) return MVSV_E_INVALID_ARG;
+    (void)hipSetDevice(ctx->device);
+    int rc = check_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    if (rc) return rc;
+    for (int i = 0; i < n; i++) {
+        if (ms) ms[i] = 0.0;
+        if (launches) launches[i] = 0;
+    }
+    for (auto& m : ctx->marks) {
+        if (m.stage >= n) continue;
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, m.a, m.b) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;
+        }
+        if (ms) ms[m.stage] += t;
+        if (launches) launches[m.stage] += 1;
+    }
+    return MVSV_OK;
+}
+
 void mvsv_destroy(mvsv_ctx* ctx)
 {
     if (!ctx) return;
     mvsv_trim(ctx);
+    mvsv_profile_reset(ctx);
+    for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
     delete ctx;
 }

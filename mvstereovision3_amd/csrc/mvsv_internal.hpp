@@ -6,6 +6,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../../include/mvsv.h"
 
@@ -64,6 +65,14 @@ struct mvsv_ctx {
     mvsv::DevBuf bm_lf, bm_rf, bm_cost;
     // host-pointer staging
     mvsv::DevBuf h_left, h_right, h_out;
+    // stage profiling (HIP events on the context stream)
+    int prof = 0;
+    struct Mark {
+        int stage;
+        hipEvent_t a, b;
+    };
+    std::vector<Mark> marks;
+    std::vector<hipEvent_t> event_pool;
 };
 
 namespace mvsv {
@@ -71,6 +80,17 @@ namespace mvsv {
 int set_error(mvsv_ctx* ctx, int code, const std::string& msg);
 int ensure(mvsv_ctx* ctx, DevBuf& b, size_t bytes, const char* what);
 int check_hip(mvsv_ctx* ctx, hipError_t e, const char* what);
+
+enum Stage { kStagePre = 0, kStageCost, kStageFixup, kStagePath, kStageFinal, kStagePost, kStageBm };
+// RAII: records a start / stop event pair around the launches in its scope
+// when profiling is enabled (no-op otherwise).
+struct StageTimer {
+    mvsv_ctx* ctx;
+    int stage;
+    hipEvent_t a = nullptr, b = nullptr;
+    StageTimer(mvsv_ctx* c, int s);
+    ~StageTimer();
+};
 
 // Device pipelines (defined in the .hip translation units). All enqueue on
 // ctx->stream. Strides are in elements.

@@ -55,17 +55,25 @@ __global__ __launch_bounds__(256) void median3x3_kernel(const int16_t* __restric
 }
 
 // ---- speckle filter: union-find ----------------------------------------------
+// Lock-free union-find in the style of ECL-CC: roots are linked towards the
+// smaller index with atomicMin (parent pointers only ever decrease and always
+// stay inside their component), find() halves paths with atomicMin as well, so
+// concurrent unions can never lose a link.  Parent words are read with
+// agent-scope relaxed atomics (L1-bypassing): other workgroups rewrite them
+// inside the same launch.
 __device__ __forceinline__ int uf_load(const int* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ int uf_find(const int* parent, int i)
+__device__ __forceinline__ int uf_find(int* parent, int i)
 {
     int p = uf_load(parent + i);
     while (p != i) {
+        int gp = uf_load(parent + p);
+        if (gp != p) atomicMin(parent + i, gp);  // path halving, never increases
         i = p;
-        p = uf_load(parent + i);
+        p = gp;
     }
     return i;
 }
@@ -83,7 +91,7 @@ __device__ void uf_unite(int* parent, int a, int b)
         }
         int old = atomicMin(parent + b, a);  // link root b under a (a < b)
         if (old == b) return;
-        b = old;  // b was re-linked concurrently: retry from its new parent
+        b = old;  // b was re-linked concurrently: continue with its new parent
     }
 }
 
@@ -121,22 +129,39 @@ __global__ __launch_bounds__(256) void speckle_merge_kernel(const int16_t* __res
     }
 }
 
+// Flatten every valid pixel onto its root and count component sizes.  Lanes
+// of a wave that share a root add once (ballot aggregation); a root whose
+// count already exceeds max_size is no longer incremented -- only
+// "size <= max_size" is ever tested, and a skip needs max_size + 1 prior adds.
 __global__ __launch_bounds__(256) void speckle_count_kernel(const int16_t* __restrict__ img,
                                                             size_t st, size_t fs, int W, int H,
-                                                            int new_val, int* __restrict__ parent,
+                                                            int new_val, int max_size,
+                                                            int* __restrict__ parent,
                                                             int* __restrict__ size)
 {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
     const int f = blockIdx.z;
-    if (x >= W || y >= H) return;
-    const int v = img[f * fs + (size_t)y * st + x];
-    if (v == new_val) return;
+    const int lane = threadIdx.x & 63;
     int* par = parent + (size_t)f * W * H;
-    const int i = y * W + x;
-    const int r = uf_find(par, i);
-    par[i] = r;  // compression: only ever points at the root
-    atomicAdd(size + (size_t)f * W * H + r, 1);
+    int* sz = size + (size_t)f * W * H;
+    int r = -1;
+    if (x < W && y < H && img[f * fs + (size_t)y * st + x] != new_val) {
+        const int i = y * W + x;
+        r = uf_find(par, i);
+        par[i] = r;
+    }
+    bool pending = r >= 0;
+    for (;;) {
+        unsigned long long m = __ballot(pending);
+        if (m == 0ull) break;
+        const int leader = __ffsll((long long)m) - 1;
+        const int r0 = __builtin_amdgcn_readlane(r, leader);
+        const unsigned long long same = __ballot(pending && r == r0);
+        if (lane == leader && uf_load(sz + r0) <= max_size)
+            atomicAdd(sz + r0, __popcll(same));
+        if (r == r0) pending = false;
+    }
 }
 
 __global__ __launch_bounds__(256) void speckle_apply_kernel(int16_t* __restrict__ img, size_t st,
@@ -221,7 +246,7 @@ int speckle_device(mvsv_ctx* ctx, int n, int16_t* img, size_t st, size_t fs, int
     hipLaunchKernelGGL(speckle_merge_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val,
                        max_diff, parent);
     hipLaunchKernelGGL(speckle_count_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val,
-                       parent, size);
+                       max_size, parent, size);
     hipLaunchKernelGGL(speckle_apply_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val,
                        max_size, parent, size);
     return check_hip(ctx, hipGetLastError(), "speckle filter");

@@ -72,31 +72,41 @@ __global__ __launch_bounds__(256) void sgbm_prefilter_kernel(
 // ---------------------------------------------------------------------------
 // 2. cost volume.
 // Block = 256 threads owns cost columns [x0, x0+TX) x rows [y0, y0+TY) x all d.
-// For each (clamped) source row it stages the BT intervals of the needed left /
-// right columns in LDS, computes the pixel cost of TX + 2*SW2 columns, the
-// horizontal box sum of its cells, and keeps the vertical window sum of its
-// cells in registers (ring of the last 2*SH2+1 horizontal sums in LDS).
+// Thread (cl, p) works on the disparity pair (2p, 2p+1) packed in one VGPR
+// (v_pk_*_u16) and on column lane cl.  For each clamped source row:
+//   stage  BT intervals of the needed left columns and (x-reversed, twice,
+//          with a one-column shift so every pair is one aligned 16-byte LDS
+//          read) right columns in LDS;
+//   pix    Birchfield-Tomasi cost of TX + 2*SW2 columns, two disparities per
+//          instruction (bytes -> u16 halves with v_perm_b32);
+//   hsum   horizontal box sum, sliding along the thread's run of RUN columns;
+//   vsum   vertical window sum kept in registers, the last 2*SH2+1 horizontal
+//          sums in an LDS ring; emit C = P2 + window sum (u16 wrap = int16 cast).
 // ---------------------------------------------------------------------------
+constexpr int kCostRun = 4;  // output columns per thread
+
 struct CostLayout {
-    int TX, TY, NX, NR, nLmax, nRmax;
-    size_t off_r, off_pix, off_ring, bytes;
+    int PP, CL, TX, TY, NX, NR, nLmax, nRmax;
+    size_t off_ra, off_rb, off_pix, off_ring, bytes;
 };
 
-__host__ __device__ inline CostLayout cost_layout(int D, int SW2, int SH2, int CPT, int TY)
+__host__ __device__ inline CostLayout cost_layout(int D, int SW2, int SH2, int TY)
 {
     CostLayout c;
-    c.TX = (256 * CPT) / D;
-    if (c.TX < 1) c.TX = 1;
+    c.PP = D / 2;
+    c.CL = 256 / c.PP;
+    if (c.CL < 1) c.CL = 1;
+    c.TX = c.CL * kCostRun;
     c.TY = TY;
     c.NX = c.TX + 2 * SW2;
     c.NR = 2 * SH2 + 1;
     c.nLmax = c.NX;
-    c.nRmax = c.NX + D;
-    c.off_r = (size_t)c.nLmax * 8;
-    c.off_pix = c.off_r + (size_t)c.nRmax * 8;
-    size_t pix = (size_t)c.NX * D * 2;
-    c.off_ring = (c.off_pix + pix + 15) & ~(size_t)15;
-    c.bytes = c.off_ring + (size_t)c.NR * c.TX * D * 2;
+    c.nRmax = c.NX + D + 2;
+    c.off_ra = ((size_t)c.nLmax * 8 + 15) & ~(size_t)15;
+    c.off_rb = c.off_ra + (((size_t)c.nRmax * 8 + 15) & ~(size_t)15);
+    c.off_pix = c.off_rb + (((size_t)c.nRmax * 8 + 15) & ~(size_t)15);
+    c.off_ring = c.off_pix + (((size_t)c.NX * c.PP * 4 + 15) & ~(size_t)15);
+    c.bytes = c.off_ring + (size_t)c.NR * c.TX * c.PP * 4;
     return c;
 }
 
@@ -110,44 +120,77 @@ __device__ __forceinline__ uint32_t bt_pack(const uint8_t* row, int x, int W)
     return (uint32_t)v | ((uint32_t)lo << 8) | ((uint32_t)hi << 16);
 }
 
-__device__ __forceinline__ int bt_cost(uint32_t a, uint32_t b)
+__device__ __forceinline__ uint32_t pk_subsat_u16(uint32_t a, uint32_t b)
 {
-    int u = a & 255, u0 = (a >> 8) & 255, u1 = (a >> 16) & 255;
-    int v = b & 255, v0 = (b >> 8) & 255, v1 = (b >> 16) & 255;
-    int c0 = max(max(0, u - v1), v0 - u);
-    int c1 = max(max(0, v - u1), u0 - v);
-    return min(c0, c1);
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, a),
+                                                                      __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
 }
 
-template <int CPT>
+// BT cost of one channel for a disparity pair: u* broadcast, v* per half.
+__device__ __forceinline__ uint32_t bt_pair(uint32_t u, uint32_t u0, uint32_t u1, uint32_t v,
+                                           uint32_t v0, uint32_t v1)
+{
+    uint32_t c0 = pk_max_u16(pk_subsat_u16(u, v1), pk_subsat_u16(v0, u));
+    uint32_t c1 = pk_max_u16(pk_subsat_u16(v, u1), pk_subsat_u16(u0, v));
+    return pk_min_u16(c0, c1);
+}
+
 __global__ __launch_bounds__(256) void sgbm_cost_kernel(const uint8_t* __restrict__ pre, int W,
                                                         int H, SgbmEff e, int TY,
                                                         int16_t* __restrict__ C)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int D = e.D, W1 = e.W1, SW2 = e.SW2, SH2 = e.SH2;
-    const CostLayout lay = cost_layout(D, SW2, SH2, CPT, TY);
-    const int TX = lay.TX, NX = lay.NX, NR = lay.NR;
+    const CostLayout lay = cost_layout(D, SW2, SH2, TY);
+    const int PP = lay.PP, CL = lay.CL, TX = lay.TX, NX = lay.NX, NR = lay.NR;
     const int f = blockIdx.z;
     const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
     const int y1 = min(y0 + TY, H);
     const int xclo = max(x0 - SW2, 0), xchi = min(x0 + TX + SW2 - 1, W1 - 1);
     const int nL = xchi - xclo + 1;
-    const int ilo = e.minX1 + xclo;                  // first left image column
-    const int rlo = ilo - (e.maxD - 1);              // first right image column
-    const int nR = (e.minX1 + xchi - e.minD) - rlo + 1;
+    const int ilo = e.minX1 + xclo;  // first left image column
+    // right columns, x-reversed: j = rtop - xr, rtop = right column of d = 0 at xc = xchi
+    const int rtop = e.minX1 + xchi - e.minD;
+    const int nR = nL + D;  // covers j in [0, nL - 1 + D - 1] (+1 slack for copy B)
     uint64_t* lpk = (uint64_t*)smem;
-    uint64_t* rpk = (uint64_t*)(smem + lay.off_r);
-    int16_t* pixrow = (int16_t*)(smem + lay.off_pix);
-    int16_t* ring = (int16_t*)(smem + lay.off_ring);
+    uint64_t* ra = (uint64_t*)(smem + lay.off_ra);
+    uint64_t* rb = (uint64_t*)(smem + lay.off_rb);
+    uint32_t* pixrow = (uint32_t*)(smem + lay.off_pix);
+    uint32_t* ring = (uint32_t*)(smem + lay.off_ring);
     const size_t plane = (size_t)W * H;
     const uint8_t* P = pre + (size_t)f * 4 * plane;
     const int tid = threadIdx.x;
-    const int ncell = TX * D;
+    const int cl = tid / PP, p = tid - (tid / PP) * PP;
+    const bool worker = cl < CL;
+    const int tx0 = cl * kCostRun;
+    const uint32_t p2x2 = (uint32_t)(e.P2 & 0xffff) * 0x10001u;
 
-    int csum[CPT];
+    uint32_t csum[kCostRun];
 #pragma unroll
-    for (int i = 0; i < CPT; i++) csum[i] = 0;
+    for (int i = 0; i < kCostRun; i++) csum[i] = 0;
 
     const int vstart = y0 - SH2, vend = y1 + SH2;
     for (int v = vstart; v < vend; v++) {
@@ -160,48 +203,72 @@ __global__ __launch_bounds__(256) void sgbm_cost_kernel(const uint8_t* __restric
             int x = ilo + i;
             lpk[i] = (uint64_t)bt_pack(Ls, x, W) | ((uint64_t)bt_pack(Lr, x, W) << 32);
         }
-        for (int i = tid; i < nR; i += 256) {
-            int x = rlo + i;
+        for (int j = tid; j <= nR; j += 256) {
+            int x = rtop - j;
             uint64_t val = 0;
             if (x >= 0 && x < W)
                 val = (uint64_t)bt_pack(Rs, x, W) | ((uint64_t)bt_pack(Rr, x, W) << 32);
-            rpk[i] = val;
+            if (j < nR) ra[j] = val;
+            if (j > 0) rb[j - 1] = val;
         }
         __syncthreads();
-        for (int idx = tid; idx < NX * D; idx += 256) {
-            int xv = idx / D;
-            int d = idx - xv * D;
-            int xc = clampi(x0 - SW2 + xv, 0, W1 - 1);
-            int li = xc - xclo;
-            int rj = (e.minX1 + xc - (d + e.minD)) - rlo;
-            uint64_t a = lpk[li], b = rpk[rj];
-            int pc = bt_cost((uint32_t)a, (uint32_t)b) +
-                     (bt_cost((uint32_t)(a >> 32), (uint32_t)(b >> 32)) >> 2);
-            pixrow[idx] = (int16_t)pc;
-        }
-        __syncthreads();
-        const int k = v - vstart;
-        const int slot = k % NR;
-        const bool emit = k >= NR - 1;
-        const int y = v - SH2;
-#pragma unroll
-        for (int i = 0; i < CPT; i++) {
-            int cell = tid + 256 * i;
-            if (cell < ncell) {
-                int tx = cell / D;
-                int d = cell - tx * D;
-                int h = 0;
-                const int16_t* pr = pixrow + tx * D + d;
-                for (int q = 0; q <= 2 * SW2; q++) h += pr[q * D];
-                int16_t* rs = ring + slot * ncell + cell;
-                if (k >= NR) csum[i] -= *rs;
-                csum[i] += h;
-                *rs = (int16_t)h;
-                if (emit && x0 + tx < W1)
-                    C[(((size_t)f * H + y) * W1 + x0 + tx) * D + d] = (int16_t)(e.P2 + csum[i]);
+        if (worker) {
+            for (int xv = cl; xv < NX; xv += CL) {
+                const int xc = clampi(x0 - SW2 + xv, 0, W1 - 1);
+                const uint64_t lw = lpk[xc - xclo];
+                const uint32_t l0 = (uint32_t)lw, l1 = (uint32_t)(lw >> 32);
+                // j of d = 2p at this column
+                const int j0 = (xchi - xc) + 2 * p;
+                const uint64_t* src = (j0 & 1) ? (rb + (j0 - 1)) : (ra + j0);
+                const uint4 rr = *(const uint4*)src;  // cols j0, j0+1 (both channels)
+                uint32_t acc;
+                {
+                    const uint32_t a = rr.x, b = rr.z;  // channel 0 of d, d+1
+                    uint32_t U = __builtin_amdgcn_perm(l0, l0, 0x0c040c00u);
+                    uint32_t U0 = __builtin_amdgcn_perm(l0, l0, 0x0c050c01u);
+                    uint32_t U1 = __builtin_amdgcn_perm(l0, l0, 0x0c060c02u);
+                    uint32_t V = __builtin_amdgcn_perm(b, a, 0x0c040c00u);
+                    uint32_t V0 = __builtin_amdgcn_perm(b, a, 0x0c050c01u);
+                    uint32_t V1 = __builtin_amdgcn_perm(b, a, 0x0c060c02u);
+                    acc = bt_pair(U, U0, U1, V, V0, V1);
+                }
+                {
+                    const uint32_t a = rr.y, b = rr.w;  // channel 1 (raw) of d, d+1
+                    uint32_t U = __builtin_amdgcn_perm(l1, l1, 0x0c040c00u);
+                    uint32_t U0 = __builtin_amdgcn_perm(l1, l1, 0x0c050c01u);
+                    uint32_t U1 = __builtin_amdgcn_perm(l1, l1, 0x0c060c02u);
+                    uint32_t V = __builtin_amdgcn_perm(b, a, 0x0c040c00u);
+                    uint32_t V0 = __builtin_amdgcn_perm(b, a, 0x0c050c01u);
+                    uint32_t V1 = __builtin_amdgcn_perm(b, a, 0x0c060c02u);
+                    uint32_t c = bt_pair(U, U0, U1, V, V0, V1);
+                    acc = pk_add_u16(acc, (c >> 2) & 0x3fff3fffu);
+                }
+                pixrow[xv * PP + p] = acc;
             }
         }
         __syncthreads();
+        if (worker) {
+            const int k = v - vstart;
+            const int slot = k % NR;
+            const bool emit = k >= NR - 1;
+            const int y = v - SH2;
+            uint32_t h = 0;
+            const uint32_t* pr = pixrow + tx0 * PP + p;
+            for (int q = 0; q <= 2 * SW2; q++) h = pk_add_u16(h, pr[q * PP]);
+#pragma unroll
+            for (int i = 0; i < kCostRun; i++) {
+                if (i > 0)
+                    h = pk_sub_u16(pk_add_u16(h, pr[(i + 2 * SW2) * PP]), pr[(i - 1) * PP]);
+                uint32_t* rs = ring + (slot * TX + tx0 + i) * PP + p;
+                if (k >= NR) csum[i] = pk_sub_u16(csum[i], *rs);
+                csum[i] = pk_add_u16(csum[i], h);
+                *rs = h;
+                const int xo = x0 + tx0 + i;
+                if (emit && xo < W1)
+                    *(uint32_t*)(C + (((size_t)f * H + y) * W1 + xo) * D + 2 * p) =
+                        pk_add_u16(p2x2, csum[i]);
+            }
+        }
     }
 }
 
@@ -577,6 +644,7 @@ int launch_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* 
         int dy = e.fullDP ? dirs_hh[k][1] : dirs_sgbm[k][1];
         int nl = num_lines(dx, dy, e.W1, H);
         dim3 grid((nl + 3) / 4, n);
+        StageTimer tm(ctx, kStagePath);
         if (k == 0)
             hipLaunchKernelGGL((sgbm_path_kernel<NP, false>), grid, dim3(256), 0, s, Cv, Sv, H,
                                e.W1, e.D, dx, dy, e.P1, e.P2);
@@ -585,6 +653,7 @@ int launch_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* 
                                e.W1, e.D, dx, dy, e.P1, e.P2);
     }
     size_t lds = (size_t)W * 3 * sizeof(int16_t);
+    StageTimer tm(ctx, kStageFinal);
     hipLaunchKernelGGL((sgbm_final_kernel<NP>), dim3(H, n), dim3(64), lds, s, Cv, Sv, H, W, e,
                        raw);
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels");
@@ -615,41 +684,34 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     int16_t* Sv = (int16_t*)ctx->agg.ptr;
     int16_t* raw = (int16_t*)ctx->raw.ptr;
 
-    hipLaunchKernelGGL(sgbm_prefilter_kernel, dim3(H, n), dim3(256), 0, s, L, ls, lfs, R, rs, rfs,
-                       W, H, e.ftzero, pre);
-
-    // cost volume: pick cells-per-thread so the LDS image stays <= 64 KiB
-    const int TY = H >= 256 ? 48 : 16;
-    int cpt = 8;
-    CostLayout lay = cost_layout(e.D, e.SW2, e.SH2, cpt, TY);
-    while (lay.bytes > 65536 && cpt > 1) {
-        cpt >>= 1;
-        lay = cost_layout(e.D, e.SW2, e.SH2, cpt, TY);
+    {
+        StageTimer tm(ctx, kStagePre);
+        hipLaunchKernelGGL(sgbm_prefilter_kernel, dim3(H, n), dim3(256), 0, s, L, ls, lfs, R, rs,
+                           rfs, W, H, e.ftzero, pre);
     }
+
+    // cost volume: one block per TX x TY tile; keep the LDS image <= 160 KiB
+    int TY = H >= 256 ? 48 : 16;
+    CostLayout lay = cost_layout(e.D, e.SW2, e.SH2, TY);
     if (lay.bytes > 160 * 1024)
         return set_error(ctx, MVSV_E_INVALID_ARG, "blockSize too large for the GPU cost kernel");
     dim3 cgrid((e.W1 + lay.TX - 1) / lay.TX, (H + TY - 1) / TY, n);
-    if (lay.bytes > 65536) {
-        const void* fn = cpt == 8 ? (const void*)sgbm_cost_kernel<8>
-                       : cpt == 4 ? (const void*)sgbm_cost_kernel<4>
-                       : cpt == 2 ? (const void*)sgbm_cost_kernel<2>
-                                  : (const void*)sgbm_cost_kernel<1>;
-        if ((rc = check_hip(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)lay.bytes),
-                            "sgbm cost LDS attribute")))
-            return rc;
-    }
-    switch (cpt) {
-    case 8: hipLaunchKernelGGL(sgbm_cost_kernel<8>, cgrid, dim3(256), lay.bytes, s, pre, W, H, e, TY, Cv); break;
-    case 4: hipLaunchKernelGGL(sgbm_cost_kernel<4>, cgrid, dim3(256), lay.bytes, s, pre, W, H, e, TY, Cv); break;
-    case 2: hipLaunchKernelGGL(sgbm_cost_kernel<2>, cgrid, dim3(256), lay.bytes, s, pre, W, H, e, TY, Cv); break;
-    default: hipLaunchKernelGGL(sgbm_cost_kernel<1>, cgrid, dim3(256), lay.bytes, s, pre, W, H, e, TY, Cv); break;
+    if (lay.bytes > 65536 &&
+        (rc = check_hip(ctx, hipFuncSetAttribute((const void*)sgbm_cost_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)lay.bytes),
+                        "sgbm cost LDS attribute")))
+        return rc;
+    {
+        StageTimer tm(ctx, kStageCost);
+        hipLaunchKernelGGL(sgbm_cost_kernel, cgrid, dim3(256), lay.bytes, s, pre, W, H, e, TY, Cv);
     }
     if ((rc = check_hip(ctx, hipGetLastError(), "sgbm cost kernel"))) return rc;
 
     const int ybot = std::max(H - e.SH2, 1);     // first row that is never recomputed
     const int ylast = std::max(H - e.SH2 - 1, 0);  // last recomputed row
     if (H > 1) {
+        StageTimer tm(ctx, kStageFixup);
         hipLaunchKernelGGL(sgbm_cost_fixup_kernel, dim3(H - 1, n), dim3(256), 0, s, Cv, H, e,
                            ylast, ybot);
         if ((rc = check_hip(ctx, hipGetLastError(), "sgbm cost fixup"))) return rc;
@@ -661,6 +723,7 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     else rc = launch_paths<4>(ctx, n, H, W, e, Cv, Sv, raw);
     if (rc) return rc;
 
+    StageTimer tm(ctx, kStagePost);
     if ((rc = median3x3_device(ctx, n, raw, W, plane, out, os, ofs, W, H))) return rc;
     if (e.speckle_window > 0)
         return speckle_device(ctx, n, out, os, ofs, W, H, e.invalid, e.speckle_window,
