@@ -53,17 +53,22 @@ def parse():
     return ap.parse_args()
 
 
-def stage_bytes(stage, F, W, H, W1, D, ndir):
-    """Algorithmic HBM bytes of one step per stage ("Kernels")."""
-    vol2 = W1 * H * D * 2
+def stage_bytes(stage, F, W, H, W1, D, ndir, acc):
+    """Algorithmic HBM bytes of one step per stage ("Kernels").
+
+    acc = bytes per (pixel, disparity) of the cross-direction delta
+    accumulator (1 when ndir * P2 <= 255, else 2).
+    """
+    cells = W1 * H * D
     px = W * H
     return {
-        "prefilter": F * (2 * px + 4 * px),
-        "cost_volume": F * (4 * px + vol2),
+        "prefilter": F * (2 * px + 2 * 8 * px),
+        "cost_volume": F * (2 * 8 * px + 2 * cells),
         "cost_fixup": 0,
-        # first direction writes S from C, the others read C, read S, write S
-        "path_aggregation": F * vol2 * (2 + 3 * (ndir - 1)),
-        "final_wta_lr": F * (2 * vol2 + 2 * px),
+        # first direction: read C, write acc; the others: read C, read + write acc
+        "path_aggregation": F * cells * ((2 + acc) + (ndir - 2) * (2 + 2 * acc)),
+        # last direction + WTA: read C and acc, write the int16 row
+        "final_wta_lr": F * (cells * (2 + acc) + 2 * px),
         "post_filters": F * 4 * px,
     }.get(stage, 0)
 
@@ -124,6 +129,9 @@ def main():
     D, minD = params["num_disparities"], params["min_disparity"]
     W1 = W - max(minD + D, 0) + min(minD, 0)
     ndir = 8 if args.mode == 1 else 5
+    P1 = params["p1"] if params["p1"] > 0 else 2
+    P2 = max(params["p2"] if params["p2"] > 0 else 5, P1 + 1)
+    acc = 1 if ndir * P2 <= 255 else 2
 
     host = [mvsv.synth_pair(SEED0 + rank * F + j, W, H, minD, D) for j in range(F)]
     Lt = torch.from_numpy(np.stack([h[0] for h in host])).to(dev)
@@ -170,7 +178,7 @@ def main():
                   for k, v in prof.items() if v[1]}
         dom = max(stages, key=lambda k: stages[k]["ms_per_step"])
         launches = stages[dom]["launches_per_step"]
-        bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir) / launches
+        bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir, acc) / launches
         avg_launch_s = stages[dom]["ms_per_step"] / launches / 1e3
         achieved = bytes_per_launch / avg_launch_s / 1e9
         traffic = None

@@ -95,38 +95,131 @@ __device__ void uf_unite(int* parent, int a, int b)
     }
 }
 
-__global__ __launch_bounds__(256) void speckle_init_kernel(int* __restrict__ parent,
-                                                           int* __restrict__ size, int npix)
+// Stage 1: union-find inside a 32x32 tile in LDS (one 256-thread block per
+// tile, 4 pixels per thread), then every pixel's global parent = its tile-local
+// root (row-major local order is monotone in the global index, so roots stay
+// the smallest index of their tile component).  Also zeroes the size array.
+constexpr int kSpTile = 32;
+
+__device__ __forceinline__ int lds_load(const int* p)
 {
-    const int f = blockIdx.y;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < npix; i += gridDim.x * 256) {
-        parent[(size_t)f * npix + i] = i;
-        size[(size_t)f * npix + i] = 0;
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ int lfind(int* par, int i)
+{
+    int p = lds_load(par + i);
+    while (p != i) {
+        int gp = lds_load(par + p);
+        if (gp != p) atomicMin(par + i, gp);
+        i = p;
+        p = gp;
+    }
+    return i;
+}
+
+__device__ void lunite(int* par, int a, int b)
+{
+    for (;;) {
+        a = lfind(par, a);
+        b = lfind(par, b);
+        if (a == b) return;
+        if (a > b) {
+            int t = a;
+            a = b;
+            b = t;
+        }
+        int old = atomicMin(par + b, a);
+        if (old == b) return;
+        b = old;
     }
 }
 
-__global__ __launch_bounds__(256) void speckle_merge_kernel(const int16_t* __restrict__ img,
+__global__ __launch_bounds__(256) void speckle_local_kernel(const int16_t* __restrict__ img,
+                                                            size_t st, size_t fs, int W, int H,
+                                                            int new_val, int max_diff,
+                                                            int* __restrict__ parent,
+                                                            int* __restrict__ size)
+{
+    __shared__ int lpar[kSpTile * kSpTile];
+    __shared__ int lval[kSpTile * kSpTile];
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    const int x0 = blockIdx.x * kSpTile, y0 = blockIdx.y * kSpTile;
+    const int f = blockIdx.z;
+    const int16_t* s = img + f * fs;
+    const int kInvalid = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int ly = ty + 8 * k, li = ly * kSpTile + tx;
+        const int gx = x0 + tx, gy = y0 + ly;
+        int v = kInvalid;
+        if (gx < W && gy < H) {
+            int t = s[(size_t)gy * st + gx];
+            if (t != new_val) v = t;
+        }
+        lval[li] = v;
+        lpar[li] = li;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int ly = ty + 8 * k, li = ly * kSpTile + tx;
+        const int v = lval[li];
+        if (v == kInvalid) continue;
+        if (tx + 1 < kSpTile) {
+            int u = lval[li + 1];
+            if (u != kInvalid && abs(v - u) <= max_diff) lunite(lpar, li, li + 1);
+        }
+        if (ly + 1 < kSpTile) {
+            int u = lval[li + kSpTile];
+            if (u != kInvalid && abs(v - u) <= max_diff) lunite(lpar, li, li + kSpTile);
+        }
+    }
+    __syncthreads();
+    int* par = parent + (size_t)f * W * H;
+    int* sz = size + (size_t)f * W * H;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int ly = ty + 8 * k, li = ly * kSpTile + tx;
+        const int gx = x0 + tx, gy = y0 + ly;
+        if (gx >= W || gy >= H) continue;
+        const int gi = gy * W + gx;
+        int g = gi;
+        if (lval[li] != kInvalid) {
+            const int r = lfind(lpar, li);
+            g = (y0 + r / kSpTile) * W + x0 + (r % kSpTile);
+        }
+        par[gi] = g;
+        sz[gi] = 0;
+    }
+}
+
+// Stage 2: unions across tile borders only (right and bottom edge of each tile).
+__global__ __launch_bounds__(64) void speckle_border_kernel(const int16_t* __restrict__ img,
                                                             size_t st, size_t fs, int W, int H,
                                                             int new_val, int max_diff,
                                                             int* __restrict__ parent)
 {
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int t = threadIdx.x;
+    const int x0 = blockIdx.x * kSpTile, y0 = blockIdx.y * kSpTile;
     const int f = blockIdx.z;
-    if (x >= W || y >= H) return;
+    int x, y, nx, ny;
+    if (t < kSpTile) {  // right edge: (x0+31, y0+t) -- (x0+32, y0+t)
+        x = x0 + kSpTile - 1;
+        y = y0 + t;
+        nx = x + 1;
+        ny = y;
+    } else {  // bottom edge: (x0+t', y0+31) -- (x0+t', y0+32)
+        x = x0 + (t - kSpTile);
+        y = y0 + kSpTile - 1;
+        nx = x;
+        ny = y + 1;
+    }
+    if (x >= W || y >= H || nx >= W || ny >= H) return;
     const int16_t* s = img + f * fs;
-    int* par = parent + (size_t)f * W * H;
-    const int v = s[(size_t)y * st + x];
-    if (v == new_val) return;
-    const int i = y * W + x;
-    if (x + 1 < W) {
-        int u = s[(size_t)y * st + x + 1];
-        if (u != new_val && abs(v - u) <= max_diff) uf_unite(par, i, i + 1);
-    }
-    if (y + 1 < H) {
-        int u = s[(size_t)(y + 1) * st + x];
-        if (u != new_val && abs(v - u) <= max_diff) uf_unite(par, i, i + W);
-    }
+    const int v = s[(size_t)y * st + x], u = s[(size_t)ny * st + nx];
+    if (v == new_val || u == new_val || abs(v - u) > max_diff) return;
+    uf_unite(parent + (size_t)f * W * H, y * W + x, ny * W + nx);
 }
 
 // Flatten every valid pixel onto its root and count component sizes.  Lanes
@@ -239,12 +332,12 @@ int speckle_device(mvsv_ctx* ctx, int n, int16_t* img, size_t st, size_t fs, int
     int* parent = (int*)ctx->uf_parent.ptr;
     int* size = (int*)ctx->uf_size.ptr;
     hipStream_t s = ctx->stream;
-    int blocks = (int)std::min<size_t>((npix + 255) / 256, 2048);
-    hipLaunchKernelGGL(speckle_init_kernel, dim3(blocks, n), dim3(256), 0, s, parent, size,
-                       (int)npix);
-    dim3 grid((W + 63) / 64, (H + 3) / 4, n);
-    hipLaunchKernelGGL(speckle_merge_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val,
+    dim3 tiles((W + kSpTile - 1) / kSpTile, (H + kSpTile - 1) / kSpTile, n);
+    hipLaunchKernelGGL(speckle_local_kernel, tiles, dim3(256), 0, s, img, st, fs, W, H, new_val,
+                       max_diff, parent, size);
+    hipLaunchKernelGGL(speckle_border_kernel, tiles, dim3(64), 0, s, img, st, fs, W, H, new_val,
                        max_diff, parent);
+    dim3 grid((W + 63) / 64, (H + 3) / 4, n);
     hipLaunchKernelGGL(speckle_count_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val,
                        max_size, parent, size);
     hipLaunchKernelGGL(speckle_apply_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val,

@@ -30,42 +30,55 @@ namespace {
 using namespace dev;
 
 // ---------------------------------------------------------------------------
-// 1. prefilter: planes [frame][4][H][W] = L sobel, L raw, R sobel, R raw.
+// 1. prefilter: per pixel one u64 = BT interval of the clipped x-Sobel channel
+//    (bits 0-23: val | lo << 8 | hi << 16) and of the raw channel (bits
+//    32-55), planes [frame][2][H][W] (left, right).
 // [OpenCV] calcPixelCostBT: tab[(r[x+1]-r[x-1])*2 + rn[x+1]-rn[x-1] + rs[x+1]-rs[x-1]],
-// columns 0 and W-1 of both channels = tab[0] = ftzero.
+// columns 0 and W-1 of both channels = tab[0] = ftzero; the BT interval of a
+// value v is min/max of {v, (v + left)/2, (v + right)/2} inside the row.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bt_interval(int v, int l, int r, bool has_l, bool has_r)
+{
+    int a = has_l ? (v + l) >> 1 : v;
+    int b = has_r ? (v + r) >> 1 : v;
+    int lo = min(min(a, b), v), hi = max(max(a, b), v);
+    return (uint32_t)v | ((uint32_t)lo << 8) | ((uint32_t)hi << 16);
+}
+
 __global__ __launch_bounds__(256) void sgbm_prefilter_kernel(
     const uint8_t* __restrict__ L, size_t ls, size_t lfs, const uint8_t* __restrict__ R,
-    size_t rs, size_t rfs, int W, int H, int ftzero, uint8_t* __restrict__ pre)
+    size_t rs, size_t rfs, int W, int H, int ftzero, uint64_t* __restrict__ pre)
 {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint8_t* ch = smem;  // [4][W]: L sobel, L raw, R sobel, R raw
     const int y = blockIdx.x;
-    const int f = blockIdx.y;
-    const uint8_t* l = L + f * lfs;
-    const uint8_t* r = R + f * rfs;
-    const size_t plane = (size_t)W * H;
-    uint8_t* o = pre + (size_t)f * 4 * plane + (size_t)y * W;
+    const int img = blockIdx.y;  // 0 = left, 1 = right
+    const int f = blockIdx.z;
+    const uint8_t* base = img == 0 ? L + f * lfs : R + f * rfs;
+    const size_t st = img == 0 ? ls : rs;
     const int yn = y > 0 ? y - 1 : y, ys = y < H - 1 ? y + 1 : y;
-    const uint8_t* l0 = l + (size_t)y * ls;
-    const uint8_t* ln = l + (size_t)yn * ls;
-    const uint8_t* lsr = l + (size_t)ys * ls;
-    const uint8_t* r0 = r + (size_t)y * rs;
-    const uint8_t* rn = r + (size_t)yn * rs;
-    const uint8_t* rsr = r + (size_t)ys * rs;
+    const uint8_t* r0 = base + (size_t)y * st;
+    const uint8_t* rn = base + (size_t)yn * st;
+    const uint8_t* rsr = base + (size_t)ys * st;
     const uint8_t fz = (uint8_t)ftzero;
     for (int x = threadIdx.x; x < W; x += blockDim.x) {
-        uint8_t a = fz, b = fz, c = fz, d = fz;
+        uint8_t a = fz, b = fz;
         if (x > 0 && x < W - 1) {
-            int gl = (l0[x + 1] - l0[x - 1]) * 2 + ln[x + 1] - ln[x - 1] + lsr[x + 1] - lsr[x - 1];
-            int gr = (r0[x + 1] - r0[x - 1]) * 2 + rn[x + 1] - rn[x - 1] + rsr[x + 1] - rsr[x - 1];
-            a = (uint8_t)(clampi(gl, -ftzero, ftzero) + ftzero);
-            b = l0[x];
-            c = (uint8_t)(clampi(gr, -ftzero, ftzero) + ftzero);
-            d = r0[x];
+            int g = (r0[x + 1] - r0[x - 1]) * 2 + rn[x + 1] - rn[x - 1] + rsr[x + 1] - rsr[x - 1];
+            a = (uint8_t)(clampi(g, -ftzero, ftzero) + ftzero);
+            b = r0[x];
         }
-        o[x] = a;
-        o[plane + x] = b;
-        o[2 * plane + x] = c;
-        o[3 * plane + x] = d;
+        ch[x] = a;
+        ch[W + x] = b;
+    }
+    __syncthreads();
+    uint64_t* o = pre + (((size_t)f * 2 + img) * H + y) * W;
+    for (int x = threadIdx.x; x < W; x += blockDim.x) {
+        const bool hl = x > 0, hr = x < W - 1;
+        const int xl = hl ? x - 1 : x, xr = hr ? x + 1 : x;
+        uint32_t s0 = bt_interval(ch[x], ch[xl], ch[xr], hl, hr);
+        uint32_t s1 = bt_interval(ch[W + x], ch[W + xl], ch[W + xr], hl, hr);
+        o[x] = (uint64_t)s0 | ((uint64_t)s1 << 32);
     }
 }
 
@@ -110,16 +123,6 @@ __host__ __device__ inline CostLayout cost_layout(int D, int SW2, int SH2, int T
     return c;
 }
 
-// BT interval of one column of one channel: val | lo << 8 | hi << 16.
-__device__ __forceinline__ uint32_t bt_pack(const uint8_t* row, int x, int W)
-{
-    int v = row[x];
-    int l = x > 0 ? (v + row[x - 1]) >> 1 : v;
-    int r = x < W - 1 ? (v + row[x + 1]) >> 1 : v;
-    int lo = min(min(l, r), v), hi = max(max(l, r), v);
-    return (uint32_t)v | ((uint32_t)lo << 8) | ((uint32_t)hi << 16);
-}
-
 __device__ __forceinline__ uint32_t pk_subsat_u16(uint32_t a, uint32_t b)
 {
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -158,7 +161,9 @@ __device__ __forceinline__ uint32_t bt_pair(uint32_t u, uint32_t u0, uint32_t u1
     return pk_min_u16(c0, c1);
 }
 
-__global__ __launch_bounds__(256) void sgbm_cost_kernel(const uint8_t* __restrict__ pre, int W,
+constexpr int kStageRegs = 3;  // staging loads per thread per row (nL + nR + 1 <= 768)
+
+__global__ __launch_bounds__(256) void sgbm_cost_kernel(const uint64_t* __restrict__ pre, int W,
                                                         int H, SgbmEff e, int TY,
                                                         int16_t* __restrict__ C)
 {
@@ -181,37 +186,58 @@ __global__ __launch_bounds__(256) void sgbm_cost_kernel(const uint8_t* __restric
     uint32_t* pixrow = (uint32_t*)(smem + lay.off_pix);
     uint32_t* ring = (uint32_t*)(smem + lay.off_ring);
     const size_t plane = (size_t)W * H;
-    const uint8_t* P = pre + (size_t)f * 4 * plane;
+    const uint64_t* PL = pre + (size_t)f * 2 * plane;
+    const uint64_t* PR = PL + plane;
     const int tid = threadIdx.x;
     const int cl = tid / PP, p = tid - (tid / PP) * PP;
     const bool worker = cl < CL;
     const int tx0 = cl * kCostRun;
     const uint32_t p2x2 = (uint32_t)(e.P2 & 0xffff) * 0x10001u;
+    // staging item i: i < nL -> left column ilo + i; else right j = i - nL (0..nR)
+    const int nItems = nL + nR + 1;
 
     uint32_t csum[kCostRun];
 #pragma unroll
     for (int i = 0; i < kCostRun; i++) csum[i] = 0;
+    uint64_t pf[kStageRegs];
+
+    auto fetch_row = [&](int v) {
+        const int r = clampi(v, 0, H - 1);
+        const uint64_t* lrow = PL + (size_t)r * W;
+        const uint64_t* rrow = PR + (size_t)r * W;
+#pragma unroll
+        for (int k = 0; k < kStageRegs; k++) {
+            const int i = tid + 256 * k;
+            uint64_t val = 0;
+            if (i < nL) {
+                val = lrow[ilo + i];
+            } else if (i < nItems) {
+                const int x = rtop - (i - nL);
+                if (x >= 0 && x < W) val = rrow[x];
+            }
+            pf[k] = val;
+        }
+    };
+    auto stage_row = [&]() {
+#pragma unroll
+        for (int k = 0; k < kStageRegs; k++) {
+            const int i = tid + 256 * k;
+            if (i < nL) {
+                lpk[i] = pf[k];
+            } else if (i < nItems) {
+                const int j = i - nL;
+                if (j < nR) ra[j] = pf[k];
+                if (j > 0) rb[j - 1] = pf[k];
+            }
+        }
+    };
 
     const int vstart = y0 - SH2, vend = y1 + SH2;
+    fetch_row(vstart);
+    stage_row();
     for (int v = vstart; v < vend; v++) {
-        const int r = clampi(v, 0, H - 1);
-        const uint8_t* Ls = P + (size_t)r * W;
-        const uint8_t* Lr = Ls + plane;
-        const uint8_t* Rs = Ls + 2 * plane;
-        const uint8_t* Rr = Ls + 3 * plane;
-        for (int i = tid; i < nL; i += 256) {
-            int x = ilo + i;
-            lpk[i] = (uint64_t)bt_pack(Ls, x, W) | ((uint64_t)bt_pack(Lr, x, W) << 32);
-        }
-        for (int j = tid; j <= nR; j += 256) {
-            int x = rtop - j;
-            uint64_t val = 0;
-            if (x >= 0 && x < W)
-                val = (uint64_t)bt_pack(Rs, x, W) | ((uint64_t)bt_pack(Rr, x, W) << 32);
-            if (j < nR) ra[j] = val;
-            if (j > 0) rb[j - 1] = val;
-        }
-        __syncthreads();
+        __syncthreads();  // staging of row v visible; hsum of row v-1 done with pixrow
+        if (v + 1 < vend) fetch_row(v + 1);  // in flight during the pixel-cost phase
         if (worker) {
             for (int xv = cl; xv < NX; xv += CL) {
                 const int xc = clampi(x0 - SW2 + xv, 0, W1 - 1);
@@ -246,7 +272,8 @@ __global__ __launch_bounds__(256) void sgbm_cost_kernel(const uint8_t* __restric
                 pixrow[xv * PP + p] = acc;
             }
         }
-        __syncthreads();
+        __syncthreads();  // pixrow complete; staging buffers free
+        if (v + 1 < vend) stage_row();
         if (worker) {
             const int k = v - vstart;
             const int slot = k % NR;
@@ -308,6 +335,12 @@ __global__ __launch_bounds__(256) void sgbm_cost_fixup_kernel(int16_t* __restric
 struct Line {
     int xs, ys, len;
 };
+
+// u8 accumulator when the summed path deltas (each <= P2) fit a byte
+__host__ __device__ inline bool acc_is_u8(const SgbmEff& e)
+{
+    return (e.fullDP ? 8 : 5) * e.P2 <= 255;
+}
 
 __device__ __forceinline__ Line line_geometry(int line, int dx, int dy, int W1, int H)
 {
@@ -410,13 +443,113 @@ __device__ __forceinline__ int lane_min(const uint32_t (&ln)[NP])
     return m;
 }
 
-constexpr int kPF = 4;  // software prefetch depth (steps)
 
-template <int NP, bool ACC>
+// Cross-direction accumulator.  With cb = C - P2 (the unbiased box cost) every
+// path cost is L_r = cb + delta_r with delta_r in [0, P2] (the min() term of
+// the recurrence minus min_k L_r(p-r,k) lies in [0, P2]); hence
+//     S = min(sum_r L_r, MAX_COST) = min(ndir*cb + sum_r delta_r, MAX_COST)
+// and only sum_r delta_r has to travel between the direction kernels: one byte
+// per (pixel, disparity) when ndir*P2 <= 255 (sgbm.yml: P2 = 5), else a
+// saturating u16 (saturation above MAX_COST cannot change the min()).
+template <int NP, typename AccT>
+struct AccVec;
+
+template <int NP>
+struct AccVec<NP, uint16_t> {  // packed u16 pairs, one dword per pair
+    static __device__ __forceinline__ void load(const uint16_t* p, uint32_t (&v)[NP])
+    {
+        Vec<NP> t;
+        t.load((const int16_t*)p);
+#pragma unroll
+        for (int i = 0; i < NP; i++) v[i] = t.v[i];
+    }
+    static __device__ __forceinline__ void store(uint16_t* p, const uint32_t (&v)[NP])
+    {
+        Vec<NP> t;
+#pragma unroll
+        for (int i = 0; i < NP; i++) t.v[i] = v[i];
+        t.store((int16_t*)p);
+    }
+    static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b)
+    {
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        return __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(
+                                                __builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+    }
+};
+
+// u8 storage: byte pair <-> u16 pair with v_perm_b32
+__device__ __forceinline__ uint32_t u8x2_to_u16x2(uint32_t w, int half)
+{
+    return __builtin_amdgcn_perm(0u, w, half ? 0x0c030c02u : 0x0c010c00u);
+}
+
+template <>
+struct AccVec<1, uint8_t> {
+    static __device__ __forceinline__ void load(const uint8_t* p, uint32_t (&v)[1])
+    {
+        v[0] = u8x2_to_u16x2(*(const uint16_t*)p, 0);
+    }
+    static __device__ __forceinline__ void store(uint8_t* p, const uint32_t (&v)[1])
+    {
+        *(uint16_t*)p = (uint16_t)__builtin_amdgcn_perm(0u, v[0], 0x0c0c0200u);
+    }
+    static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) { return a + b; }
+};
+template <>
+struct AccVec<2, uint8_t> {
+    static __device__ __forceinline__ void load(const uint8_t* p, uint32_t (&v)[2])
+    {
+        uint32_t w = *(const uint32_t*)p;
+        v[0] = u8x2_to_u16x2(w, 0);
+        v[1] = u8x2_to_u16x2(w, 1);
+    }
+    static __device__ __forceinline__ void store(uint8_t* p, const uint32_t (&v)[2])
+    {
+        *(uint32_t*)p = __builtin_amdgcn_perm(v[1], v[0], 0x06040200u);
+    }
+    static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) { return a + b; }
+};
+template <>
+struct AccVec<4, uint8_t> {
+    static __device__ __forceinline__ void load(const uint8_t* p, uint32_t (&v)[4])
+    {
+        uint2 w = *(const uint2*)p;
+        v[0] = u8x2_to_u16x2(w.x, 0);
+        v[1] = u8x2_to_u16x2(w.x, 1);
+        v[2] = u8x2_to_u16x2(w.y, 0);
+        v[3] = u8x2_to_u16x2(w.y, 1);
+    }
+    static __device__ __forceinline__ void store(uint8_t* p, const uint32_t (&v)[4])
+    {
+        *(uint2*)p = make_uint2(__builtin_amdgcn_perm(v[1], v[0], 0x06040200u),
+                                __builtin_amdgcn_perm(v[3], v[2], 0x06040200u));
+    }
+    static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) { return a + b; }
+};
+
+// delta = L - C + P2 (exact, in [0, P2]) for a packed pair
+__device__ __forceinline__ uint32_t path_delta(uint32_t ln, uint32_t c, uint32_t p2x2)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    u16x2 r = __builtin_bit_cast(u16x2, ln) - __builtin_bit_cast(u16x2, c) + __builtin_bit_cast(u16x2, p2x2);
+    return __builtin_bit_cast(uint32_t, r);
+}
+
+// One wave per scanline.  The loop is branch-free around memory: every
+// prefetch address is clamped into the line (duplicates are never consumed),
+// so the compiler can count outstanding loads exactly and keep kPathPF steps
+// of C / accumulator loads in flight.  FULL = every lane owns real
+// disparities (D == 128 * NP); otherwise stores are lane-predicated.
+constexpr int kPathPF = 8;
+
+template <int NP, bool FIRST, bool FULL, typename AccT>
 __global__ __launch_bounds__(256) void sgbm_path_kernel(const int16_t* __restrict__ C,
-                                                        int16_t* __restrict__ S, int H, int W1,
+                                                        AccT* __restrict__ A, int H, int W1,
                                                         int D, int dx, int dy, int P1, int P2)
 {
+    using AV = AccVec<NP, AccT>;
+    constexpr int PF = kPathPF;
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane keeps the line walk scalar
     const int line = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -426,66 +559,76 @@ __global__ __launch_bounds__(256) void sgbm_path_kernel(const int16_t* __restric
     const size_t frame = (size_t)H * W1 * D;
     const ptrdiff_t step = ((ptrdiff_t)dy * W1 + dx) * D;
     const int d0 = lane * 2 * NP;
-    const size_t off = f * frame + ((size_t)g.ys * W1 + g.xs) * D + (d0 < D ? d0 : 0);
+    const bool lane_on = FULL || d0 < D;
+    const size_t off = f * frame + ((size_t)g.ys * W1 + g.xs) * D + (lane_on ? d0 : 0);
     const int16_t* cp = C + off;
-    int16_t* sp = S + off;
+    AccT* ap = A + off;
     bool valid[NP];
     uint32_t lp[NP];
 #pragma unroll
     for (int p = 0; p < NP; p++) {
-        valid[p] = d0 + 2 * p < D;
+        valid[p] = FULL || d0 + 2 * p < D;
         lp[p] = valid[p] ? 0u : 0x7fff7fffu;
     }
-    const bool lane_on = d0 < D;
     const uint32_t p1x2 = (uint32_t)(P1 & 0xffff) * 0x10001u;
+    const uint32_t p2x2 = (uint32_t)(P2 & 0xffff) * 0x10001u;
     int minp = 0;
     const int len = g.len;
 
-    Vec<NP> cb[kPF], sb[kPF];
+    Vec<NP> cb[PF];
+    uint32_t ab[PF][NP];
 #pragma unroll
-    for (int j = 0; j < kPF; j++) {
-        if (j < len && lane_on) {
-            cb[j].load(cp + j * step);
-            if (ACC) sb[j].load(sp + j * step);
+    for (int j = 0; j < PF; j++) {
+        const ptrdiff_t t = min(j, len - 1);
+        cb[j].load(cp + t * step);
+        if (!FIRST) AV::load(ap + t * step, ab[j]);
+    }
+    auto body = [&](int s, int j) {
+        const int dl = (int16_t)(minp + P2);
+        const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
+        uint32_t c[NP], ln[NP], o[NP];
+#pragma unroll
+        for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
+        sgm_step<NP>(lp, delta2, p1x2, c, valid, ln);
+        minp = wave_min_i32(lane_min<NP>(ln));
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            uint32_t dv = path_delta(ln[p], c[p], p2x2);
+            o[p] = FIRST ? dv : AV::add(ab[j][p], dv);
+            lp[p] = ln[p];
+        }
+        if (FULL || lane_on) AV::store(ap + (ptrdiff_t)s * step, o);
+    };
+    int s = 0;
+    for (; s + PF <= len; s += PF) {
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            body(s + j, j);
+            const ptrdiff_t t = min(s + j + PF, len - 1);
+            cb[j].load(cp + t * step);
+            if (!FIRST) AV::load(ap + t * step, ab[j]);
         }
     }
-    for (int base = 0; base < len; base += kPF) {
+    const int rem = len - s;
 #pragma unroll
-        for (int j = 0; j < kPF; j++) {
-            const int s = base + j;
-            if (s >= len) break;
-            const int dl = (int16_t)(minp + P2);
-            const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
-            uint32_t c[NP], ln[NP];
-#pragma unroll
-            for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
-            sgm_step<NP>(lp, delta2, p1x2, c, valid, ln);
-            minp = wave_min_i32(lane_min<NP>(ln));
-            if (lane_on) {
-                Vec<NP> o;
-#pragma unroll
-                for (int p = 0; p < NP; p++) o.v[p] = ACC ? pk_add_sat(sb[j].v[p], ln[p]) : ln[p];
-                o.store(sp + (ptrdiff_t)s * step);
-                if (s + kPF < len) {
-                    cb[j].load(cp + (ptrdiff_t)(s + kPF) * step);
-                    if (ACC) sb[j].load(sp + (ptrdiff_t)(s + kPF) * step);
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < NP; p++) lp[p] = ln[p];
-        }
-    }
+    for (int j = 0; j < PF; j++)
+        if (j < rem) body(s + j, j);
 }
 
 // ---------------------------------------------------------------------------
 // 5. last direction (R->L) + WTA + uniqueness + sub-pixel + LR check.
 // ---------------------------------------------------------------------------
-template <int NP>
+constexpr int kFinalPF = 4;
+
+template <int NP, bool FULL, typename AccT>
 __global__ __launch_bounds__(64) void sgbm_final_kernel(const int16_t* __restrict__ C,
-                                                       const int16_t* __restrict__ S, int H,
+                                                       const AccT* __restrict__ A, int H,
                                                        int W, SgbmEff e,
                                                        int16_t* __restrict__ raw)
 {
+    using AV = AccVec<NP, AccT>;
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    constexpr int PF = kFinalPF;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int16_t* disp1 = (int16_t*)smem;
     int16_t* d2 = disp1 + W;
@@ -505,109 +648,135 @@ __global__ __launch_bounds__(64) void sgbm_final_kernel(const int16_t* __restric
     const bool lane_rule = !e.fullDP && !(e.variant & MVSV_VARIANT_WTA_MIN_D);
     const size_t frame = (size_t)H * W1 * D;
     const int d0 = lane * 2 * NP;
-    const bool lane_on = d0 < D;
+    const bool lane_on = FULL || d0 < D;
     const size_t off = f * frame + ((size_t)y * W1 + (W1 - 1)) * D + (lane_on ? d0 : 0);
     const int16_t* cp = C + off;
-    const int16_t* sp = S + off;
+    const AccT* sp = A + off;
     bool valid[NP];
     uint32_t lp[NP];
 #pragma unroll
     for (int p = 0; p < NP; p++) {
-        valid[p] = d0 + 2 * p < D;
+        valid[p] = FULL || d0 + 2 * p < D;
         lp[p] = valid[p] ? 0u : 0x7fff7fffu;
     }
     const uint32_t p1x2 = (uint32_t)(e.P1 & 0xffff) * 0x10001u;
+    const uint32_t p2x2 = (uint32_t)(e.P2 & 0xffff) * 0x10001u;
+    const bool eight = e.fullDP != 0;
     int minp = 0;
     const int uq = e.uniq;
 
-    Vec<NP> cb[kPF], sb[kPF];
+    Vec<NP> cb[PF];
+    uint32_t sb[PF][NP];
 #pragma unroll
-    for (int j = 0; j < kPF; j++) {
-        if (j < W1 && lane_on) {
-            cb[j].load(cp - (ptrdiff_t)j * D);
-            sb[j].load(sp - (ptrdiff_t)j * D);
-        }
+    for (int j = 0; j < PF; j++) {
+        const ptrdiff_t t = min(j, W1 - 1);
+        cb[j].load(cp - t * D);
+        AV::load(sp - t * D, sb[j]);
     }
-    for (int base = 0; base < W1; base += kPF) {
+    // phase A of one step: recurrence, total cost, WTA reductions (no LDS, no
+    // branches); results per step: minS, best, rejected, Sm, Sp (wave-uniform)
+    int rMin[PF], rBest[PF], rRej[PF], rSm[PF], rSp[PF];
+    auto phaseA = [&](int j) {
+        const int dl = (int16_t)(minp + e.P2);
+        const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
+        uint32_t c[NP], ln[NP], st[NP];
 #pragma unroll
-        for (int j = 0; j < kPF; j++) {
-            const int s = base + j;
-            if (s >= W1) break;
-            const int x = W1 - 1 - s;
-            const int dl = (int16_t)(minp + e.P2);
-            const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
-            uint32_t c[NP], ln[NP], st[NP];
+        for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
+        sgm_step<NP>(lp, delta2, p1x2, c, valid, ln);
+        minp = wave_min_i32(lane_min<NP>(ln));
+        int key = 0x7fffffff;
 #pragma unroll
-            for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
-            sgm_step<NP>(lp, delta2, p1x2, c, valid, ln);
-            minp = wave_min_i32(lane_min<NP>(ln));
-            // total aggregated cost and the WTA key of this lane
-            int key = 0x7fffffff;
+        for (int p = 0; p < NP; p++) {
+            // S = min(ndir*(C - P2) + sum of deltas, MAX_COST), saturating u16
+            u16x2 cbv = __builtin_bit_cast(u16x2, c[p]) - __builtin_bit_cast(u16x2, p2x2);
+            u16x2 x2 = __builtin_elementwise_add_sat(cbv, cbv);
+            u16x2 x4 = __builtin_elementwise_add_sat(x2, x2);
+            u16x2 t = eight ? __builtin_elementwise_add_sat(x4, x4)
+                            : __builtin_elementwise_add_sat(x4, cbv);
+            u16x2 acc = __builtin_elementwise_add_sat(
+                __builtin_bit_cast(u16x2, sb[j][p]),
+                __builtin_bit_cast(u16x2, path_delta(ln[p], c[p], p2x2)));
+            u16x2 sv = __builtin_elementwise_min(__builtin_elementwise_add_sat(t, acc),
+                                                 (u16x2){32767, 32767});
+            st[p] = valid[p] ? __builtin_bit_cast(uint32_t, sv) : 0x7fff7fffu;
+            lp[p] = ln[p];
 #pragma unroll
-            for (int p = 0; p < NP; p++) {
-                st[p] = valid[p] ? pk_add_sat(sb[j].v[p], ln[p]) : 0x7fff7fffu;
-                if (valid[p]) {
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        int d = d0 + 2 * p + h;
-                        int sv = h ? hi16(st[p]) : lo16(st[p]);
-                        int sub = lane_rule ? (((d & 7) << 12) | (d >> 3)) : d;
-                        key = min(key, (sv << 16) | sub);
-                    }
-                }
+            for (int h = 0; h < 2; h++) {
+                int d = d0 + 2 * p + h;
+                int v = h ? hi16(st[p]) : lo16(st[p]);
+                int sub = lane_rule ? (((d & 7) << 12) | (d >> 3)) : d;
+                key = min(key, valid[p] ? ((v << 16) | sub) : 0x7fffffff);
             }
-            if (lane_on && s + kPF < W1) {
-                cb[j].load(cp - (ptrdiff_t)(s + kPF) * D);
-                sb[j].load(sp - (ptrdiff_t)(s + kPF) * D);
-            }
-#pragma unroll
-            for (int p = 0; p < NP; p++) lp[p] = ln[p];
-
-            const int K = wave_min_i32(key);
-            const int minS = K >> 16;
-            const int sub = K & 0xffff;
-            int best = lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
-            if (minS >= kMaxCost) best = -1;  // no strict minimum below MAX_COST
-            // uniqueness: some d with S[d]*(100-u) < minS*100 and |d-best| > 1
-            bool rej = false;
-#pragma unroll
-            for (int p = 0; p < NP; p++) {
-                if (valid[p]) {
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        int d = d0 + 2 * p + h;
-                        int sv = h ? hi16(st[p]) : lo16(st[p]);
-                        rej |= (sv * (100 - uq) < minS * 100) && (abs(best - d) > 1);
-                    }
-                }
-            }
-            if (__ballot(rej) != 0ull) continue;
-            // right-view map (x descending: the larger x wins ties)
-            const int x2 = x + minX1 - best - minD;
-            if (lane == 0 && x2 >= 0 && x2 < W && d2c[x2] > minS) {
-                d2c[x2] = (int16_t)minS;
-                d2[x2] = (int16_t)(best + minD);
-            }
-            int d16;
-            if (0 < best && best < D - 1) {
-                auto fetch = [&](int d) -> int {
-                    int ln_ = d / (2 * NP), el = d - ln_ * 2 * NP;
-                    uint32_t v = st[0];
-#pragma unroll
-                    for (int p = 1; p < NP; p++)
-                        if ((el >> 1) == p) v = st[p];
-                    uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)v, ln_);
-                    return (el & 1) ? hi16(w) : lo16(w);
-                };
-                int Sm = fetch(best - 1), Sp = fetch(best + 1);
-                int den = max(Sm + Sp - 2 * minS, 1);
-                d16 = best * kDispScale + ((Sm - Sp) * kDispScale + den) / (den * 2);
-            } else {
-                d16 = best * kDispScale;
-            }
-            if (lane == 0) disp1[x + minX1] = (int16_t)(d16 + minD * kDispScale);
         }
+        const int K = wave_min_i32(key);
+        const int minS = K >> 16;
+        const int sub = K & 0xffff;
+        int best = lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
+        if (minS >= kMaxCost) best = -1;  // no strict minimum below MAX_COST
+        bool rej = false;
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                int d = d0 + 2 * p + h;
+                int v = h ? hi16(st[p]) : lo16(st[p]);
+                rej |= valid[p] && (v * (100 - uq) < minS * 100) && (abs(best - d) > 1);
+            }
+        }
+        auto fetch = [&](int d) -> int {
+            d = clampi(d, 0, D - 1);
+            int ln_ = d / (2 * NP), el = d - ln_ * 2 * NP;
+            uint32_t v = st[0];
+#pragma unroll
+            for (int p = 1; p < NP; p++) v = ((el >> 1) == p) ? st[p] : v;
+            uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)v, ln_);
+            return (el & 1) ? hi16(w) : lo16(w);
+        };
+        rMin[j] = minS;
+        rBest[j] = best;
+        rRej[j] = __ballot(rej) != 0ull;
+        rSm[j] = fetch(best - 1);
+        rSp[j] = fetch(best + 1);
+    };
+    // phase B of one step (x descending, sequential semantics of the scan)
+    auto phaseB = [&](int s, int j) {
+        if (rRej[j]) return;
+        const int x = W1 - 1 - s;
+        const int minS = rMin[j], best = rBest[j];
+        const int x2 = x + minX1 - best - minD;
+        if (lane == 0 && x2 >= 0 && x2 < W && d2c[x2] > minS) {
+            d2c[x2] = (int16_t)minS;
+            d2[x2] = (int16_t)(best + minD);
+        }
+        int d16;
+        if (0 < best && best < D - 1) {
+            const int Sm = rSm[j], Sp = rSp[j];
+            const int den = max(Sm + Sp - 2 * minS, 1);
+            d16 = best * kDispScale + ((Sm - Sp) * kDispScale + den) / (den * 2);
+        } else {
+            d16 = best * kDispScale;
+        }
+        if (lane == 0) disp1[x + minX1] = (int16_t)(d16 + minD * kDispScale);
+    };
+    int s = 0;
+    for (; s + PF <= W1; s += PF) {
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            phaseA(j);
+            const ptrdiff_t t = min(s + j + PF, W1 - 1);
+            cb[j].load(cp - t * D);
+            AV::load(sp - t * D, sb[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < PF; j++) phaseB(s + j, j);
     }
+    const int rem = W1 - s;
+#pragma unroll
+    for (int j = 0; j < PF; j++)
+        if (j < rem) phaseA(j);
+#pragma unroll
+    for (int j = 0; j < PF; j++)
+        if (j < rem) phaseB(s + j, j);
     __syncthreads();
     int16_t* out = raw + ((size_t)f * H + y) * W;
     for (int x = lane; x < W; x += 64) {
@@ -631,9 +800,9 @@ __global__ void fill_s16_kernel(int16_t* __restrict__ out, size_t os, size_t ofs
     for (int x = threadIdx.x; x < W; x += blockDim.x) o[x] = v;
 }
 
-template <int NP>
-int launch_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv,
-                 int16_t* Sv, int16_t* raw)
+template <int NP, typename AccT>
+int launch_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, AccT* Av,
+                 int16_t* raw)
 {
     hipStream_t s = ctx->stream;
     static const int dirs_sgbm[4][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}};
@@ -645,18 +814,37 @@ int launch_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* 
         int nl = num_lines(dx, dy, e.W1, H);
         dim3 grid((nl + 3) / 4, n);
         StageTimer tm(ctx, kStagePath);
-        if (k == 0)
-            hipLaunchKernelGGL((sgbm_path_kernel<NP, false>), grid, dim3(256), 0, s, Cv, Sv, H,
-                               e.W1, e.D, dx, dy, e.P1, e.P2);
+        const bool full = e.D == 128 * NP;
+        if (k == 0 && full)
+            hipLaunchKernelGGL((sgbm_path_kernel<NP, true, true, AccT>), grid, dim3(256), 0, s,
+                               Cv, Av, H, e.W1, e.D, dx, dy, e.P1, e.P2);
+        else if (k == 0)
+            hipLaunchKernelGGL((sgbm_path_kernel<NP, true, false, AccT>), grid, dim3(256), 0, s,
+                               Cv, Av, H, e.W1, e.D, dx, dy, e.P1, e.P2);
+        else if (full)
+            hipLaunchKernelGGL((sgbm_path_kernel<NP, false, true, AccT>), grid, dim3(256), 0, s,
+                               Cv, Av, H, e.W1, e.D, dx, dy, e.P1, e.P2);
         else
-            hipLaunchKernelGGL((sgbm_path_kernel<NP, true>), grid, dim3(256), 0, s, Cv, Sv, H,
-                               e.W1, e.D, dx, dy, e.P1, e.P2);
+            hipLaunchKernelGGL((sgbm_path_kernel<NP, false, false, AccT>), grid, dim3(256), 0, s,
+                               Cv, Av, H, e.W1, e.D, dx, dy, e.P1, e.P2);
     }
     size_t lds = (size_t)W * 3 * sizeof(int16_t);
     StageTimer tm(ctx, kStageFinal);
-    hipLaunchKernelGGL((sgbm_final_kernel<NP>), dim3(H, n), dim3(64), lds, s, Cv, Sv, H, W, e,
-                       raw);
+    if (e.D == 128 * NP)
+        hipLaunchKernelGGL((sgbm_final_kernel<NP, true, AccT>), dim3(H, n), dim3(64), lds, s, Cv,
+                           Av, H, W, e, raw);
+    else
+        hipLaunchKernelGGL((sgbm_final_kernel<NP, false, AccT>), dim3(H, n), dim3(64), lds, s, Cv,
+                           Av, H, W, e, raw);
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels");
+}
+
+template <int NP>
+int launch_paths_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv,
+                     void* Av, int16_t* raw)
+{
+    if (acc_is_u8(e)) return launch_paths<NP, uint8_t>(ctx, n, H, W, e, Cv, (uint8_t*)Av, raw);
+    return launch_paths<NP, uint16_t>(ctx, n, H, W, e, Cv, (uint16_t*)Av, raw);
 }
 
 }  // namespace
@@ -675,24 +863,28 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     if (e.D > 512) return set_error(ctx, MVSV_E_INVALID_ARG, "numDisparities > 512 not supported");
     const size_t plane = (size_t)W * H;
     const size_t vol = (size_t)e.W1 * H * e.D;
-    if ((rc = ensure(ctx, ctx->pre, (size_t)n * 4 * plane, "sgbm prefilter planes"))) return rc;
+    if ((rc = ensure(ctx, ctx->pre, (size_t)n * 2 * plane * 8, "sgbm BT interval planes"))) return rc;
     if ((rc = ensure(ctx, ctx->cost, (size_t)n * vol * 2, "sgbm cost volume"))) return rc;
-    if ((rc = ensure(ctx, ctx->agg, (size_t)n * vol * 2, "sgbm aggregated cost"))) return rc;
+    if ((rc = ensure(ctx, ctx->agg, (size_t)n * vol * (acc_is_u8(e) ? 1 : 2),
+                     "sgbm path-delta accumulator")))
+        return rc;
     if ((rc = ensure(ctx, ctx->raw, (size_t)n * plane * 2, "sgbm raw disparity"))) return rc;
-    uint8_t* pre = (uint8_t*)ctx->pre.ptr;
+    uint64_t* pre = (uint64_t*)ctx->pre.ptr;
     int16_t* Cv = (int16_t*)ctx->cost.ptr;
-    int16_t* Sv = (int16_t*)ctx->agg.ptr;
+    void* Sv = ctx->agg.ptr;
     int16_t* raw = (int16_t*)ctx->raw.ptr;
 
     {
         StageTimer tm(ctx, kStagePre);
-        hipLaunchKernelGGL(sgbm_prefilter_kernel, dim3(H, n), dim3(256), 0, s, L, ls, lfs, R, rs,
-                           rfs, W, H, e.ftzero, pre);
+        hipLaunchKernelGGL(sgbm_prefilter_kernel, dim3(H, 2, n), dim3(256), (size_t)W * 2, s, L,
+                           ls, lfs, R, rs, rfs, W, H, e.ftzero, pre);
     }
 
     // cost volume: one block per TX x TY tile; keep the LDS image <= 160 KiB
-    int TY = H >= 256 ? 48 : 16;
+    int TY = H >= 512 ? 96 : (H >= 256 ? 48 : 16);
     CostLayout lay = cost_layout(e.D, e.SW2, e.SH2, TY);
+    if (lay.nLmax + lay.nRmax + 1 > 256 * kStageRegs)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "numDisparities too large for the GPU cost kernel");
     if (lay.bytes > 160 * 1024)
         return set_error(ctx, MVSV_E_INVALID_ARG, "blockSize too large for the GPU cost kernel");
     dim3 cgrid((e.W1 + lay.TX - 1) / lay.TX, (H + TY - 1) / TY, n);
@@ -718,9 +910,9 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     }
 
     const int np = (e.D + 127) / 128;
-    if (np == 1) rc = launch_paths<1>(ctx, n, H, W, e, Cv, Sv, raw);
-    else if (np == 2) rc = launch_paths<2>(ctx, n, H, W, e, Cv, Sv, raw);
-    else rc = launch_paths<4>(ctx, n, H, W, e, Cv, Sv, raw);
+    if (np == 1) rc = launch_paths_acc<1>(ctx, n, H, W, e, Cv, Sv, raw);
+    else if (np == 2) rc = launch_paths_acc<2>(ctx, n, H, W, e, Cv, Sv, raw);
+    else rc = launch_paths_acc<4>(ctx, n, H, W, e, Cv, Sv, raw);
     if (rc) return rc;
 
     StageTimer tm(ctx, kStagePost);
