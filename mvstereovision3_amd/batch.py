@@ -1,0 +1,58 @@
+"""Frame-parallel batch mode (BASELINE config 4).
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI on the
+MI355X node).  Rectified pairs are independent units: frame i of the global
+batch lives on rank i // frames_per_rank and is generated / computed there; no
+collective touches the data path until the final gather of the int16 maps to
+the destination rank, the only exchange step of the reference's pipeline.
+
+The per-rank compute is injected (``compute(L, R, out)``), so the same driver
+runs the HIP path in bench.py and the CPU oracle in the world_size-2 gloo test.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence
+
+SEED0 = 0x5EED0000
+
+
+def frame_seeds(rank: int, world: int, frames_per_rank: int, seed0: int = SEED0) -> List[int]:
+    """Seeds of the frames owned by ``rank`` (contiguous block of the global batch)."""
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    return [seed0 + rank * frames_per_rank + j for j in range(frames_per_rank)]
+
+
+def global_frame_index(rank: int, j: int, frames_per_rank: int) -> int:
+    return rank * frames_per_rank + j
+
+
+def gather_frames(out, rank: int, world: int, dst: int = 0) -> Optional[list]:
+    """Gather every rank's (F, H, W) int16 block on ``dst`` (list indexed by rank)."""
+    if world == 1:
+        return [out]
+    import torch
+    import torch.distributed as dist
+    # int16 maps travel as bytes: neither gloo nor RCCL/NCCL has an int16 type
+    raw = out.contiguous().view(torch.uint8)
+    buf = [torch.empty_like(raw) for _ in range(world)] if rank == dst else None
+    dist.gather(raw, buf, dst=dst)
+    return [b.view(out.dtype) for b in buf] if buf is not None else None
+
+
+class FrameBatch:
+    """Holds one rank's frames and runs compute + gather per step."""
+
+    def __init__(self, left, right, out, compute: Callable, rank: int = 0, world: int = 1,
+                 gather: bool = True, dst: int = 0):
+        self.left, self.right, self.out = left, right, out
+        self.compute = compute
+        self.rank, self.world, self.dst = rank, world, dst
+        self.gather = gather and world > 1
+        self.gathered: Optional[Sequence] = None
+
+    def step(self):
+        self.compute(self.left, self.right, self.out)
+        if self.gather:
+            self.gathered = gather_frames(self.out, self.rank, self.world, self.dst)
+        return self.gathered

@@ -245,3 +245,63 @@ def test_invalid_params_raise(gpu, mvsv):
         mvsv.StereoSGBM.create(0, 24, 5).compute(L, R)  # numDisparities % 16 != 0
     with pytest.raises(mvsv.MvsvError):
         mvsv.StereoBM.create(16, 4).compute(L, R)  # even block size
+
+
+# ------------------------------------------------------ golden fixtures ----
+def _fixtures():
+    import json
+    import os
+    from tests.conftest import GOLDEN
+    return (np.load(os.path.join(GOLDEN, "fixtures.npz")),
+            json.load(open(os.path.join(GOLDEN, "fixtures.json"))))
+
+
+def test_golden_fixtures_sgbm_bm(gpu, mvsv):
+    """Committed vectors (tests/golden/make_golden.py), no oracle in the loop."""
+    fix, meta = _fixtures()
+    for case in meta["sgbm"]:
+        p = case["params"]
+        m = mvsv.StereoSGBM.create(p["min_disparity"], p["num_disparities"], p["block_size"],
+                                   p["p1"], p["p2"], p["disp12_max_diff"], p["pre_filter_cap"],
+                                   p["uniqueness_ratio"], p["speckle_window_size"],
+                                   p["speckle_range"], p["mode"])
+        m.setVariant(case["variant"])
+        got = m.compute(fix[case["name"] + "_L"], fix[case["name"] + "_R"])
+        want = fix[case["name"] + "_out"]
+        assert np.array_equal(got, want), case["name"] + ": " + report(got, want)
+    for case in meta["bm"]:
+        p = case["params"]
+        m = mvsv.StereoBM.create(p["num_disparities"], p["block_size"])
+        for k, v in p.items():
+            setattr(m._params, k, v)
+        got = m.compute(fix[case["name"] + "_L"], fix[case["name"] + "_R"])
+        want = fix[case["name"] + "_out"]
+        assert np.array_equal(got, want), case["name"] + ": " + report(got, want)
+
+
+def test_golden_mean_grid(gpu, mvsv):
+    torch = gpu
+    fix, _ = _fixtures()
+    got = mvsv.mean_disparity_grid(torch.from_numpy(fix["post_in"]).cuda()).cpu().numpy()
+    assert np.array_equal(got, fix["post_grid"])
+
+
+@pytest.mark.slow
+def test_size_independent_properties_full_batch(gpu, mvsv):
+    """Full-size batch (bench workload, 8 x 1280x960, D=128, 8 paths): batch result
+    equals per-frame results, is deterministic across runs, and disparities lie in
+    the valid range or are INVALID."""
+    torch = gpu
+    frames = [mvsv.synth_pair(SEED0 + i, 1280, 960, 1, 128) for i in range(8)]
+    Lt = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
+    Rt = torch.from_numpy(np.stack([f[1] for f in frames])).cuda()
+    m = mvsv.StereoSGBM.create(1, 128, 13, 0, 0, 0, 0, 0, 150, 2, mvsv.MODE_HH)
+    a = m.compute(Lt, Rt).cpu().numpy()
+    b = m.compute(Lt, Rt).cpu().numpy()
+    assert np.array_equal(a, b)
+    single = m.compute(Lt[5], Rt[5]).cpu().numpy()
+    assert np.array_equal(a[5], single)
+    valid = a != 0  # INVALID = (minD - 1) * 16 = 0
+    assert (a[valid] >= 16).all() and (a[valid] <= 128 * 16 + 16).all()
+    # the rectangle of the synthetic field sits at round(0.6 * D) = 77
+    assert abs(np.median(a[:, 400:560, 500:800]) / 16 - 77) < 1

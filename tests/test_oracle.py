@@ -1,0 +1,173 @@
+"""CPU oracle checks (no GPU): golden fixtures, the two-restatement cross-check
+and known-answer tests.  The oracle restates OpenCV 3.4 (third-party, absent
+here): parity is unpinned, so agreement between the loop-structured C oracle
+and the closed-form numpy twin is the transcription check.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests.conftest import GOLDEN
+
+FIX = np.load(os.path.join(GOLDEN, "fixtures.npz"))
+META = json.load(open(os.path.join(GOLDEN, "fixtures.json")))
+
+
+@pytest.mark.parametrize("case", META["sgbm"], ids=lambda c: c["name"])
+def test_sgbm_fixtures(oracle, case):
+    n = case["name"]
+    got = oracle.sgbm(FIX[n + "_L"], FIX[n + "_R"], case["params"], flags=case["variant"])
+    assert np.array_equal(got, FIX[n + "_out"])
+
+
+@pytest.mark.parametrize("case", META["bm"], ids=lambda c: c["name"])
+def test_bm_fixtures(oracle, case):
+    n = case["name"]
+    got = oracle.bm(FIX[n + "_L"], FIX[n + "_R"], case["params"])
+    assert np.array_equal(got, FIX[n + "_out"])
+
+
+def test_twin_reproduces_fixtures():
+    from oracle import twin
+    for case in META["sgbm"][:3]:
+        n = case["name"]
+        got = twin.sgbm_compute(FIX[n + "_L"], FIX[n + "_R"], case["params"], case["variant"])
+        assert np.array_equal(got, FIX[n + "_out"]), n
+    for case in META["bm"]:
+        n = case["name"]
+        assert np.array_equal(twin.bm_compute(FIX[n + "_L"], FIX[n + "_R"], case["params"]),
+                              FIX[n + "_out"]), n
+
+
+def test_cost_volume_fixture(oracle):
+    from oracle import twin
+    p = META["costvol_params"]
+    C = oracle.sgbm_cost_volume(FIX["costvol_L"], FIX["costvol_R"], p)
+    assert np.array_equal(C, FIX["costvol_C"])
+    assert np.array_equal(twin.sgbm_cost_volume(FIX["costvol_L"], FIX["costvol_R"], p),
+                          FIX["costvol_C"])
+
+
+def test_post_fixtures(oracle):
+    d = FIX["post_in"]
+    assert np.array_equal(oracle.median3x3(d), FIX["post_median"])
+    assert np.array_equal(oracle.filter_speckles(d, 0, 20, 16), FIX["post_speckle"])
+    assert np.array_equal(oracle.mean_disparity_grid(d), FIX["post_grid"])
+
+
+def _rand_pair(rng, H, W, shift, kind):
+    if kind == 0:
+        from scipy.ndimage import uniform_filter
+        L = uniform_filter(rng.integers(0, 256, (H, W)).astype(float), 3).round().astype(np.uint8)
+    elif kind == 1:
+        L = (rng.integers(0, 4, (H, W)) * 60).astype(np.uint8)
+        L[:, W // 3:W // 2] = 128
+    else:
+        L = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    R = np.roll(L, -shift, axis=1)
+    R = np.clip(R.astype(int) + rng.integers(-2, 3, R.shape), 0, 255).astype(np.uint8)
+    return L, R
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_cross_check_sgbm(oracle, seed):
+    from oracle import twin
+    rng = np.random.default_rng(seed)
+    H, W = int(rng.integers(12, 40)), int(rng.integers(40, 80))
+    D = int(rng.choice([16, 32]))
+    p = dict(min_disparity=int(rng.integers(-5, 5)), num_disparities=D,
+             block_size=int(rng.choice([0, 1, 3, 5, 7, 9])),
+             p1=int(rng.choice([0, 2, 72, 300])), p2=int(rng.choice([0, 5, 288, 4000])),
+             disp12_max_diff=int(rng.integers(-1, 4)),
+             pre_filter_cap=int(rng.choice([0, 15, 31, 63])),
+             uniqueness_ratio=int(rng.choice([-1, 0, 5, 15])),
+             speckle_window_size=int(rng.choice([0, 10, 50])),
+             speckle_range=int(rng.choice([1, 2, 4])), mode=int(rng.integers(0, 2)))
+    if W + min(p["min_disparity"], 0) - max(p["min_disparity"] + D, 0) <= 5:
+        p["num_disparities"] = 16
+    L, R = _rand_pair(rng, H, W, int(rng.integers(0, 16)), int(rng.integers(0, 3)))
+    flags = int(rng.integers(0, 4))
+    assert np.array_equal(oracle.sgbm(L, R, p, flags), twin.sgbm_compute(L, R, p, flags))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_cross_check_bm(oracle, seed):
+    from oracle import twin
+    rng = np.random.default_rng(100 + seed)
+    H, W = int(rng.integers(24, 60)), int(rng.integers(60, 110))
+    bs = int(rng.choice([5, 7, 9, 11, 21]))
+    if bs >= min(H, W):
+        bs = 5
+    p = dict(pre_filter_type=1, pre_filter_size=9, pre_filter_cap=int(rng.integers(1, 64)),
+             block_size=bs, min_disparity=int(rng.integers(-4, 4)),
+             num_disparities=int(rng.choice([16, 32])),
+             texture_threshold=int(rng.choice([0, 10, 100])),
+             uniqueness_ratio=int(rng.choice([0, 10, 15])),
+             speckle_window_size=int(rng.choice([0, 10])), speckle_range=int(rng.choice([0, 4, 32])),
+             disp12_max_diff=int(rng.choice([-1, 0, 1, 3])))
+    L, R = _rand_pair(rng, H, W, int(rng.integers(0, 16)), int(rng.integers(0, 3)))
+    assert np.array_equal(oracle.bm(L, R, p), twin.bm_compute(L, R, p))
+
+
+# ------------------------------------------------------ known answers -----
+def _random_dot(H, W, shift, seed=7):
+    rng = np.random.default_rng(seed)
+    L = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    R = np.zeros_like(L)
+    R[:, : W - shift] = L[:, shift:]
+    R[:, W - shift:] = rng.integers(0, 256, (H, shift))
+    return L, R
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_known_answer_sgbm_constant_shift(oracle, mode):
+    d_true = 7
+    L, R = _random_dot(48, 96, d_true)
+    p = dict(min_disparity=0, num_disparities=16, block_size=5, p1=200, p2=800, disp12_max_diff=1,
+             pre_filter_cap=31, uniqueness_ratio=10, speckle_window_size=0, speckle_range=0,
+             mode=mode)
+    d = oracle.sgbm(L, R, p)
+    inner = d[8:-8, 24:-8]
+    assert ((inner.astype(int) + 8) >> 4 == d_true).mean() > 0.99
+
+
+def test_known_answer_bm_constant_shift(oracle):
+    d_true = 11
+    L, R = _random_dot(64, 128, d_true)
+    p = dict(pre_filter_type=1, pre_filter_size=9, pre_filter_cap=31, block_size=9,
+             min_disparity=0, num_disparities=32, texture_threshold=10, uniqueness_ratio=15,
+             speckle_window_size=0, speckle_range=0, disp12_max_diff=-1)
+    d = oracle.bm(L, R, p)
+    inner = d[8:-8, 40:-8]
+    assert ((inner.astype(int) + 8) >> 4 == d_true).mean() > 0.99
+
+
+def test_constant_image_bm_all_filtered(oracle):
+    L = np.full((40, 80), 100, np.uint8)
+    p = dict(pre_filter_type=1, pre_filter_size=9, pre_filter_cap=31, block_size=9,
+             min_disparity=0, num_disparities=16, texture_threshold=10, uniqueness_ratio=15,
+             speckle_window_size=0, speckle_range=0, disp12_max_diff=-1)
+    assert (oracle.bm(L, L, p) == -16).all()
+
+
+def test_sgbm_no_columns_all_invalid(oracle):
+    L = np.zeros((20, 40), np.uint8)
+    p = dict(min_disparity=2, num_disparities=48, block_size=5, p1=0, p2=0, disp12_max_diff=0,
+             pre_filter_cap=0, uniqueness_ratio=0, speckle_window_size=0, speckle_range=0, mode=0)
+    assert (oracle.sgbm(L, L, p) == 16).all()  # INVALID = (minD - 1) * 16
+
+
+def test_sgbm_saturated_costs_invalid(oracle):
+    """All S saturate at MAX_COST -> no strict minimum -> bestDisp = -1 -> INVALID."""
+    from oracle import twin
+    rng = np.random.default_rng(3)
+    L = rng.integers(0, 256, (16, 77)).astype(np.uint8)
+    R = np.roll(L, -5, axis=1)
+    p = dict(min_disparity=-4, num_disparities=16, block_size=11, p1=0, p2=4000,
+             disp12_max_diff=-1, pre_filter_cap=63, uniqueness_ratio=0, speckle_window_size=0,
+             speckle_range=1, mode=1)
+    a = oracle.sgbm(L, R, p, core_only=True)
+    assert np.array_equal(a, twin.sgbm_core(L, R, p))
+    assert (a == -80).any()
