@@ -135,9 +135,12 @@ MVSV_API int mvsv_bm_validate(const mvsv_bm_params* p, int W, int H);
 MVSV_API int mvsv_create(mvsv_ctx** out, int hip_device);
 MVSV_API void mvsv_destroy(mvsv_ctx* ctx);
 MVSV_API const char* mvsv_last_error(const mvsv_ctx* ctx);
-/* Use an external hipStream_t (e.g. the caller's current stream); NULL restores
- * the context's own stream. */
+/* Enqueue on an external hipStream_t (e.g. the caller's current stream).
+ * NULL selects the HIP null (default) stream, which is what torch's default
+ * current stream is; mvsv_use_own_stream() returns to the context's own
+ * non-blocking stream. */
 MVSV_API int mvsv_set_stream(mvsv_ctx* ctx, void* hip_stream);
+MVSV_API int mvsv_use_own_stream(mvsv_ctx* ctx);
 MVSV_API void* mvsv_get_stream(mvsv_ctx* ctx);
 MVSV_API int mvsv_synchronize(mvsv_ctx* ctx);
 /* Release cached device buffers. */

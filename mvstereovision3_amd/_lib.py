@@ -97,6 +97,7 @@ def _declare(lib):
         "mvsv_destroy": ([P], None),
         "mvsv_last_error": ([P], ctypes.c_char_p),
         "mvsv_set_stream": ([P, P], I),
+        "mvsv_use_own_stream": ([P], I),
         "mvsv_get_stream": ([P], P),
         "mvsv_synchronize": ([P], I),
         "mvsv_trim": ([P], I),

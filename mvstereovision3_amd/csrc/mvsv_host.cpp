@@ -346,7 +346,14 @@ const char* mvsv_last_error(const mvsv_ctx* ctx) { return ctx ? ctx->err.c_str()
 int mvsv_set_stream(mvsv_ctx* ctx, void* s)
 {
     if (!ctx) return MVSV_E_INVALID_ARG;
-    ctx->stream = s ? (hipStream_t)s : ctx->own;
+    ctx->stream = (hipStream_t)s;  // NULL = the HIP null stream
+    return MVSV_OK;
+}
+
+int mvsv_use_own_stream(mvsv_ctx* ctx)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    ctx->stream = ctx->own;
     return MVSV_OK;
 }
 

@@ -82,6 +82,7 @@ def _run_host(fn, params, left, right, out, what):
             or out.dtype != np.int16 or out.strides[1] != 2:
         out = np.empty((H, W), np.int16)  # cv::Mat::create semantics: reallocate
     ctx = context(0)
+    check(lib().mvsv_use_own_stream(ctx.handle), ctx.handle)
     rc = fn(ctx.handle, L.ctypes.data, L.strides[0], R.ctypes.data, R.strides[0], W, H,
             ctypes.byref(params), out.ctypes.data, out.strides[0] // 2)
     check(rc, ctx.handle)
