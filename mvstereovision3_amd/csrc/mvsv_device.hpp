@@ -45,6 +45,35 @@ __device__ __forceinline__ uint32_t wave_shl1(uint32_t v, uint32_t edge)
     return (uint32_t)__builtin_amdgcn_update_dpp((int)edge, (int)v, 0x130, 0xf, 0xf, false);
 }
 
+// Shifts by one lane inside each 16-lane DPP row (row_shr:1 / row_shl:1); the
+// lane of a row that has no source keeps `edge`.
+__device__ __forceinline__ uint32_t row_shr1(uint32_t v, uint32_t edge)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)edge, (int)v, 0x111, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t row_shl1(uint32_t v, uint32_t edge)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)edge, (int)v, 0x101, 0xf, 0xf, false);
+}
+
+// Minimum / maximum over each 16-lane row; every lane of the row gets the result.
+__device__ __forceinline__ int row_min_i32(int v)
+{
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, false));  // row_mirror
+    return v;
+}
+__device__ __forceinline__ int row_max_i32(int v)
+{
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, false));
+    return v;
+}
+
 // Minimum over the 64 lanes, returned wave-uniform (scalar).  DPP butterfly
 // inside each 16-lane row, then the four row results through readlane.
 __device__ __forceinline__ int wave_min_i32(int v)

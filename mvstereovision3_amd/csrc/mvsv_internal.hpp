@@ -60,7 +60,8 @@ struct mvsv_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // SGBM
-    mvsv::DevBuf pre, cost, agg, raw, uf_parent, uf_size;
+    mvsv::DevBuf pre, cost, agg, raw, uf_parent, uf_size, dummy, keys;
+    int path16 = 1;  // 16-lanes-per-scanline path kernels where D allows
     // BM
     mvsv::DevBuf bm_lf, bm_rf, bm_cost;
     // host-pointer staging

@@ -410,6 +410,22 @@ struct Vec<4> {
     }
 };
 
+template <>
+struct Vec<8> {
+    uint32_t v[8];
+    __device__ __forceinline__ void load(const int16_t* p)
+    {
+        uint4 a = *(const uint4*)p, b = *(const uint4*)(p + 8);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+    __device__ __forceinline__ void store(int16_t* p) const
+    {
+        *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
+        *(uint4*)(p + 8) = make_uint4(v[4], v[5], v[6], v[7]);
+    }
+};
+
 // One SGM step for the NP packed pairs a lane owns.  lp: previous L (MAX in
 // padded slots), delta = (int16)(minLp + P2) packed twice, c: cost C.
 template <int NP>
@@ -528,6 +544,30 @@ struct AccVec<4, uint8_t> {
     static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) { return a + b; }
 };
 
+template <>
+struct AccVec<8, uint8_t> {
+    static __device__ __forceinline__ void load(const uint8_t* p, uint32_t (&v)[8])
+    {
+        uint4 w = *(const uint4*)p;
+        v[0] = u8x2_to_u16x2(w.x, 0);
+        v[1] = u8x2_to_u16x2(w.x, 1);
+        v[2] = u8x2_to_u16x2(w.y, 0);
+        v[3] = u8x2_to_u16x2(w.y, 1);
+        v[4] = u8x2_to_u16x2(w.z, 0);
+        v[5] = u8x2_to_u16x2(w.z, 1);
+        v[6] = u8x2_to_u16x2(w.w, 0);
+        v[7] = u8x2_to_u16x2(w.w, 1);
+    }
+    static __device__ __forceinline__ void store(uint8_t* p, const uint32_t (&v)[8])
+    {
+        *(uint4*)p = make_uint4(__builtin_amdgcn_perm(v[1], v[0], 0x06040200u),
+                                __builtin_amdgcn_perm(v[3], v[2], 0x06040200u),
+                                __builtin_amdgcn_perm(v[5], v[4], 0x06040200u),
+                                __builtin_amdgcn_perm(v[7], v[6], 0x06040200u));
+    }
+    static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) { return a + b; }
+};
+
 // delta = L - C + P2 (exact, in [0, P2]) for a packed pair
 __device__ __forceinline__ uint32_t path_delta(uint32_t ln, uint32_t c, uint32_t p2x2)
 {
@@ -613,6 +653,295 @@ __global__ __launch_bounds__(256) void sgbm_path_kernel(const int16_t* __restric
 #pragma unroll
     for (int j = 0; j < PF; j++)
         if (j < rem) body(s + j, j);
+}
+
+// ---------------------------------------------------------------------------
+// 4b. path aggregation, 16 lanes per scanline (D = 32 * NP, NP in {1,2,4,8}).
+// A wave walks four scanlines at once, one per 16-lane DPP row: every lane
+// owns 2*NP consecutive disparities (16 B of C per lane for D = 128), the d+-1
+// neighbours cross lanes with row_shr/row_shl, the per-step min over d is a
+// four-step DPP butterfly inside the row (no readlane / SGPR round trip).
+// Rows whose scanline is shorter than the wave's longest one keep running on
+// clamped loads and store into a private dummy slot (branch-free memory).
+// ---------------------------------------------------------------------------
+template <int NP>
+__device__ __forceinline__ void sgm_step_row(const uint32_t (&lp)[NP], uint32_t delta2,
+                                             uint32_t p1x2, const uint32_t (&c)[NP],
+                                             uint32_t (&ln)[NP])
+{
+    const uint32_t MAXP = 0x7fff7fffu;
+    const uint32_t prev_hi = row_shr1(lp[NP - 1], MAXP);
+    const uint32_t next_lo = row_shl1(lp[0], MAXP);
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+        uint32_t ph = p == 0 ? prev_hi : lp[p - 1];
+        uint32_t nl = p == NP - 1 ? next_lo : lp[p + 1];
+        uint32_t lm = __builtin_amdgcn_alignbit(lp[p], ph, 16);
+        uint32_t lq = __builtin_amdgcn_alignbit(nl, lp[p], 16);
+        uint32_t m = pk_min(lp[p], pk_add_sat(lm, p1x2));
+        m = pk_min(m, pk_add_sat(lq, p1x2));
+        m = pk_min(m, delta2);
+        ln[p] = pk_add_sat(pk_sub_sat(m, delta2), c[p]);
+    }
+}
+
+template <int NP>
+__device__ __forceinline__ int lane_min_row(const uint32_t (&ln)[NP])
+{
+    uint32_t m = ln[0];
+#pragma unroll
+    for (int p = 1; p < NP; p++) m = pk_min(m, ln[p]);
+    return min(lo16(m), hi16(m));
+}
+
+constexpr int kPath16PF = 8;
+
+template <int NP, bool FIRST, typename AccT>
+__global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restrict__ C,
+                                                          AccT* __restrict__ A,
+                                                          AccT* __restrict__ dummy, int H, int W1,
+                                                          int D, int dx, int dy, int P1, int P2)
+{
+    using AV = AccVec<NP, AccT>;
+    constexpr int PF = kPath16PF;
+    const int lane = threadIdx.x & 63;
+    const int row = lane >> 4, rl = lane & 15;
+    const int nl = num_lines(dx, dy, W1, H);
+    const int line0 = __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + (threadIdx.x >> 6)) * 4);
+    if (line0 >= nl) return;
+    const int f = blockIdx.y;
+    const int line = min(line0 + row, nl - 1);
+    const Line g = line_geometry(line, dx, dy, W1, H);
+    const int len = line0 + row < nl ? g.len : 0;
+    const int maxlen = max(max(__builtin_amdgcn_readlane(len, 0), __builtin_amdgcn_readlane(len, 16)),
+                           max(__builtin_amdgcn_readlane(len, 32), __builtin_amdgcn_readlane(len, 48)));
+    const size_t frame = (size_t)H * W1 * D;
+    const ptrdiff_t step = ((ptrdiff_t)dy * W1 + dx) * D;
+    const int d0 = rl * 2 * NP;
+    const size_t off = f * frame + ((size_t)g.ys * W1 + g.xs) * D + d0;
+    const int16_t* cp = C + off;
+    AccT* ap = A + off;
+    AccT* dp = dummy + (size_t)threadIdx.x * 2 * NP;
+    const int last = max(len - 1, 0);
+    uint32_t lp[NP];
+#pragma unroll
+    for (int p = 0; p < NP; p++) lp[p] = 0u;
+    const uint32_t p1x2 = (uint32_t)(P1 & 0xffff) * 0x10001u;
+    const uint32_t p2x2 = (uint32_t)(P2 & 0xffff) * 0x10001u;
+    int minp = 0;
+
+    Vec<NP> cb[PF];
+    uint32_t ab[PF][NP];
+#pragma unroll
+    for (int j = 0; j < PF; j++) {
+        const ptrdiff_t t = min(j, last);
+        cb[j].load(cp + t * step);
+        if (!FIRST) AV::load(ap + t * step, ab[j]);
+    }
+    auto body = [&](int s, int j) {
+        const int dl = (int16_t)(minp + P2);
+        const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
+        uint32_t c[NP], ln[NP], o[NP];
+#pragma unroll
+        for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
+        sgm_step_row<NP>(lp, delta2, p1x2, c, ln);
+        minp = row_min_i32(lane_min_row<NP>(ln));
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            uint32_t dv = path_delta(ln[p], c[p], p2x2);
+            o[p] = FIRST ? dv : AV::add(ab[j][p], dv);
+            lp[p] = ln[p];
+        }
+        AccT* dst = s < len ? ap + (ptrdiff_t)s * step : dp;
+        AV::store(dst, o);
+    };
+    int s = 0;
+    for (; s + PF <= maxlen; s += PF) {
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            body(s + j, j);
+            const ptrdiff_t t = min(s + j + PF, last);
+            cb[j].load(cp + t * step);
+            if (!FIRST) AV::load(ap + t * step, ab[j]);
+        }
+    }
+    const int rem = maxlen - s;
+#pragma unroll
+    for (int j = 0; j < PF; j++)
+        if (j < rem) body(s + j, j);
+}
+
+// ---------------------------------------------------------------------------
+// 5b. last direction (R->L) + WTA + uniqueness + sub-pixel + LR check with 16
+// lanes per image row (4 rows per wave).  The right-view map is built with
+// order-independent atomicMin on keys (minS << 16 | 0xFFFF - x): smallest cost,
+// then the largest x -- exactly OpenCV's descending scan with a strict '>'.
+// ---------------------------------------------------------------------------
+constexpr int kFinal16PF = 4;
+
+template <int NP, typename AccT>
+__global__ __launch_bounds__(64) void sgbm_final16_kernel(const int16_t* __restrict__ C,
+                                                         const AccT* __restrict__ A, int H, int W,
+                                                         SgbmEff e, int16_t* __restrict__ raw,
+                                                         uint32_t* __restrict__ keys)
+{
+    using AV = AccVec<NP, AccT>;
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    constexpr int PF = kFinal16PF;
+    const int lane = threadIdx.x;
+    const int row = lane >> 4, rl = lane & 15;
+    const int yr = blockIdx.x * 4 + row;
+    const bool exists = yr < H;
+    const int y = min(yr, H - 1);
+    const int f = blockIdx.y;
+    const int D = e.D, W1 = e.W1, minD = e.minD, minX1 = e.minX1;
+    const int INV = e.invalid;
+    int16_t* orow = raw + ((size_t)f * H + y) * W;
+    uint32_t* krow = keys + ((size_t)f * H + y) * W;
+    if (exists)
+        for (int x = rl; x < W; x += 16) {
+            orow[x] = (int16_t)INV;
+            krow[x] = 0xffffffffu;
+        }
+    __threadfence_block();
+    __syncthreads();
+
+    const bool lane_rule = !e.fullDP && !(e.variant & MVSV_VARIANT_WTA_MIN_D);
+    const size_t frame = (size_t)H * W1 * D;
+    const int d0 = rl * 2 * NP;
+    const size_t off = f * frame + ((size_t)y * W1 + (W1 - 1)) * D + d0;
+    const int16_t* cp = C + off;
+    const AccT* sp = A + off;
+    uint32_t lp[NP];
+#pragma unroll
+    for (int p = 0; p < NP; p++) lp[p] = 0u;
+    const uint32_t p1x2 = (uint32_t)(e.P1 & 0xffff) * 0x10001u;
+    const uint32_t p2x2 = (uint32_t)(e.P2 & 0xffff) * 0x10001u;
+    const bool eight = e.fullDP != 0;
+    const int uq = e.uniq;
+    const int rowbase = lane & ~15;
+    int minp = 0;
+
+    Vec<NP> cb[PF];
+    uint32_t sb[PF][NP];
+#pragma unroll
+    for (int j = 0; j < PF; j++) {
+        const ptrdiff_t t = min(j, W1 - 1);
+        cb[j].load(cp - t * D);
+        AV::load(sp - t * D, sb[j]);
+    }
+    auto body = [&](int s, int j) {
+        const int dl = (int16_t)(minp + e.P2);
+        const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
+        uint32_t c[NP], ln[NP], st[NP];
+#pragma unroll
+        for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
+        sgm_step_row<NP>(lp, delta2, p1x2, c, ln);
+        minp = row_min_i32(lane_min_row<NP>(ln));
+        int key = 0x7fffffff;
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            // S = min(ndir*(C - P2) + sum of deltas, MAX_COST), saturating u16
+            u16x2 cbv = __builtin_bit_cast(u16x2, c[p]) - __builtin_bit_cast(u16x2, p2x2);
+            u16x2 x2v = __builtin_elementwise_add_sat(cbv, cbv);
+            u16x2 x4 = __builtin_elementwise_add_sat(x2v, x2v);
+            u16x2 t = eight ? __builtin_elementwise_add_sat(x4, x4)
+                            : __builtin_elementwise_add_sat(x4, cbv);
+            u16x2 acc = __builtin_elementwise_add_sat(
+                __builtin_bit_cast(u16x2, sb[j][p]),
+                __builtin_bit_cast(u16x2, path_delta(ln[p], c[p], p2x2)));
+            u16x2 sv = __builtin_elementwise_min(__builtin_elementwise_add_sat(t, acc),
+                                                 (u16x2){32767, 32767});
+            st[p] = __builtin_bit_cast(uint32_t, sv);
+            lp[p] = ln[p];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                int d = d0 + 2 * p + h;
+                int v = h ? hi16(st[p]) : lo16(st[p]);
+                int sub = lane_rule ? (((d & 7) << 12) | (d >> 3)) : d;
+                key = min(key, (v << 16) | sub);
+            }
+        }
+        const int K = row_min_i32(key);
+        const int minS = K >> 16;
+        const int sub = K & 0xffff;
+        int best = lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
+        if (minS >= kMaxCost) best = -1;  // no strict minimum below MAX_COST
+        int rej = 0;
+        if (uq != 0) {  // with uq == 0 the test reads S[d] < minS: never true
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    int d = d0 + 2 * p + h;
+                    int v = h ? hi16(st[p]) : lo16(st[p]);
+                    rej |= (v * (100 - uq) < minS * 100) && (abs(best - d) > 1);
+                }
+            }
+        }
+        rej = row_max_i32(rej);
+        // S[best-1], S[best+1] from the owning lanes of the row
+        auto fetch = [&](int d) -> int {
+            d = clampi(d, 0, D - 1);
+            const int owner = d / (2 * NP), el = d - owner * 2 * NP;
+            uint32_t v = st[0];
+#pragma unroll
+            for (int p = 1; p < NP; p++) v = ((el >> 1) == p) ? st[p] : v;
+            uint32_t w = (uint32_t)__shfl((int)v, rowbase + owner, 64);
+            return (el & 1) ? hi16(w) : lo16(w);
+        };
+        const int Sm = fetch(best - 1), Sp = fetch(best + 1);
+        if (rl == 0 && exists && !rej) {
+            const int x = W1 - 1 - s;
+            int d16;
+            if (0 < best && best < D - 1) {
+                const int den = max(Sm + Sp - 2 * minS, 1);
+                d16 = best * kDispScale + ((Sm - Sp) * kDispScale + den) / (den * 2);
+            } else {
+                d16 = best * kDispScale;
+            }
+            orow[x + minX1] = (int16_t)(d16 + minD * kDispScale);
+            const int x2 = x + minX1 - best - minD;
+            if (minS < kMaxCost && x2 >= 0 && x2 < W)
+                atomicMin(krow + x2, ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
+        }
+    };
+    int s = 0;
+    for (; s + PF <= W1; s += PF) {
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            body(s + j, j);
+            const ptrdiff_t t = min(s + j + PF, W1 - 1);
+            cb[j].load(cp - t * D);
+            AV::load(sp - t * D, sb[j]);
+        }
+    }
+    const int rem = W1 - s;
+#pragma unroll
+    for (int j = 0; j < PF; j++)
+        if (j < rem) body(s + j, j);
+    __threadfence_block();
+    __syncthreads();
+    if (!exists) return;
+    // left-right check (src: OpenCV 3.4 final loop) -- reads the finished row
+    for (int x = minX1 + rl; x < e.maxX1; x += 16) {
+        const int v = orow[x];
+        if (v == INV) continue;
+        const int dlo = v >> kDispShift, dhi = (v + kDispScale - 1) >> kDispShift;
+        const int xl = x - dlo, xh = x - dhi;
+        auto d2at = [&](int xx) -> int {
+            const uint32_t k = __hip_atomic_load(krow + xx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // untouched entries keep OpenCV's INVALID_DISP_SCALED (compared as a disparity)
+            if (k == 0xffffffffu) return INV;
+            const int xc = 0xffff - (int)(k & 0xffffu);
+            return xc + minX1 - xx;  // best + minD of the winning cost column
+        };
+        if (0 <= xl && xl < W && 0 <= xh && xh < W) {
+            const int a = d2at(xl), b = d2at(xh);
+            if (a >= minD && abs(a - dlo) > e.disp12 && b >= minD && abs(b - dhi) > e.disp12)
+                orow[x] = (int16_t)INV;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -801,6 +1130,37 @@ __global__ void fill_s16_kernel(int16_t* __restrict__ out, size_t os, size_t ofs
 }
 
 template <int NP, typename AccT>
+int launch_paths16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, AccT* Av,
+                   int16_t* raw)
+{
+    hipStream_t s = ctx->stream;
+    static const int dirs_sgbm[4][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}};
+    static const int dirs_hh[7][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}, {1, -1}, {0, -1}, {-1, -1}};
+    int rc;
+    if ((rc = ensure(ctx, ctx->dummy, 256 * 16 * 2, "sgbm dummy slots"))) return rc;
+    if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
+    AccT* dummy = (AccT*)ctx->dummy.ptr;
+    const int ndir = e.fullDP ? 7 : 4;
+    for (int k = 0; k < ndir; k++) {
+        int dx = e.fullDP ? dirs_hh[k][0] : dirs_sgbm[k][0];
+        int dy = e.fullDP ? dirs_hh[k][1] : dirs_sgbm[k][1];
+        int nl = num_lines(dx, dy, e.W1, H);
+        dim3 grid((nl + 15) / 16, n);
+        StageTimer tm(ctx, kStagePath);
+        if (k == 0)
+            hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT>), grid, dim3(256), 0, s, Cv, Av,
+                               dummy, H, e.W1, e.D, dx, dy, e.P1, e.P2);
+        else
+            hipLaunchKernelGGL((sgbm_path16_kernel<NP, false, AccT>), grid, dim3(256), 0, s, Cv,
+                               Av, dummy, H, e.W1, e.D, dx, dy, e.P1, e.P2);
+    }
+    StageTimer tm(ctx, kStageFinal);
+    hipLaunchKernelGGL((sgbm_final16_kernel<NP, AccT>), dim3((H + 3) / 4, n), dim3(64), 0, s, Cv,
+                       Av, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
+    return check_hip(ctx, hipGetLastError(), "sgbm path kernels (16-lane)");
+}
+
+template <int NP, typename AccT>
 int launch_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, AccT* Av,
                  int16_t* raw)
 {
@@ -837,6 +1197,14 @@ int launch_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* 
         hipLaunchKernelGGL((sgbm_final_kernel<NP, false, AccT>), dim3(H, n), dim3(64), lds, s, Cv,
                            Av, H, W, e, raw);
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels");
+}
+
+template <int NP>
+int launch_paths16_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv,
+                       void* Av, int16_t* raw)
+{
+    if (acc_is_u8(e)) return launch_paths16<NP, uint8_t>(ctx, n, H, W, e, Cv, (uint8_t*)Av, raw);
+    return launch_paths16<NP, uint16_t>(ctx, n, H, W, e, Cv, (uint16_t*)Av, raw);
 }
 
 template <int NP>
@@ -910,7 +1278,15 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     }
 
     const int np = (e.D + 127) / 128;
-    if (np == 1) rc = launch_paths_acc<1>(ctx, n, H, W, e, Cv, Sv, raw);
+    const bool wide = ctx->path16 && (e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256);
+    if (wide) {
+        switch (e.D) {
+        case 32: rc = launch_paths16_acc<1>(ctx, n, H, W, e, Cv, Sv, raw); break;
+        case 64: rc = launch_paths16_acc<2>(ctx, n, H, W, e, Cv, Sv, raw); break;
+        case 128: rc = launch_paths16_acc<4>(ctx, n, H, W, e, Cv, Sv, raw); break;
+        default: rc = launch_paths16_acc<8>(ctx, n, H, W, e, Cv, Sv, raw); break;
+        }
+    } else if (np == 1) rc = launch_paths_acc<1>(ctx, n, H, W, e, Cv, Sv, raw);
     else if (np == 2) rc = launch_paths_acc<2>(ctx, n, H, W, e, Cv, Sv, raw);
     else rc = launch_paths_acc<4>(ctx, n, H, W, e, Cv, Sv, raw);
     if (rc) return rc;
