@@ -12,7 +12,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmvsv.so")
+# MVSV_LIBRARY: an alternative in-tree build of the same ABI (A/B kernel variants)
+LIB_PATH = os.environ.get("MVSV_LIBRARY") or os.path.join(_HERE, "libmvsv.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mvsv.h")
 
 MVSV_OK = 0

@@ -257,6 +257,12 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
         return MVSV_E_HIP;
     }
     c->stream = c->own;
+    // kernel-variant switches for A/B measurement and for testing the
+    // general-shape kernels on shapes the specialised ones also cover
+    if (const char* v = std::getenv("MVSV_KERNELS")) {
+        if (std::strstr(v, "cost-lds")) c->cost2 = 0;
+        if (std::strstr(v, "path-wave")) c->path16 = 0;
+    }
     *out = c;
     return MVSV_OK;
 }

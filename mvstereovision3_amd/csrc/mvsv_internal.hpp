@@ -62,6 +62,7 @@ struct mvsv_ctx {
     // SGBM
     mvsv::DevBuf pre, cost, agg, raw, uf_parent, uf_size, dummy, keys;
     int path16 = 1;  // 16-lanes-per-scanline path kernels where D allows
+    int cost2 = 1;   // register-ring cost kernel where blockSize <= 15
     // BM
     mvsv::DevBuf bm_lf, bm_rf, bm_cost;
     // host-pointer staging

@@ -299,6 +299,243 @@ __global__ __launch_bounds__(256) void sgbm_cost_kernel(const uint64_t* __restri
     }
 }
 
+// ---------------------------------------------------------------------------
+// 2b. cost volume, register-ring variant (NR = blockSize rows, 1..15).
+// Block = 512 threads; thread (cl, p) owns disparity pair p and the RUN output
+// columns [cl*RUN, cl*RUN + RUN) of a TX = CL*RUN wide tile.  Per source row:
+//   stage  left columns as broadcast u16-pair forms {v, lo, hi} x 2 channels and
+//          right columns as (j, j+1) u16-pair forms, so one lane reads the BT
+//          operands of two disparities with two aligned 16-byte LDS reads and
+//          no byte shuffles (double-buffered: row k+1 is staged while row k is
+//          matched);
+//   pix    BT cost of TX + 2*SW2 columns;
+//   hsum   sliding horizontal box sum over the thread's RUN columns;
+//   vsum   the last NR horizontal sums live in registers (ring slot = row mod
+//          NR, resolved at compile time by unrolling the row loop by NR).
+// One workgroup barrier per row.
+// ---------------------------------------------------------------------------
+constexpr int kCost2Threads = 512;
+constexpr int kCost2Run = 4;
+
+struct Cost2Layout {
+    int PP, CL, TX, TY, NX, nQmax, qhalf;
+    size_t off_l4, off_l2, off_q4, off_q2, off_pix, bytes;
+    size_t lstride4, lstride2, qstride4, qstride2, pstride;  // bytes per buffer (x2 each)
+};
+
+// A column's BT operands for both channels are six u16-pair dwords
+// {a.v, a.lo, a.hi, b.v, b.lo, b.hi}: dwords 0-3 in a 16-byte slot (ds_read_b128,
+// 4 LDS cycles), dwords 4-5 in an 8-byte slot (ds_read_b64, 2 cycles).  Right
+// pairs j are stored by parity so the lanes of a wave (j = t + 2p) read
+// consecutive, conflict-free slots.
+__host__ __device__ inline Cost2Layout cost2_layout(int D, int SW2, int TY)
+{
+    Cost2Layout c;
+    c.PP = D / 2;
+    c.CL = kCost2Threads / c.PP;
+    c.TX = c.CL * kCost2Run;
+    c.TY = TY;
+    c.NX = c.TX + 2 * SW2;
+    c.nQmax = c.NX + D - 1;
+    c.qhalf = (c.nQmax + 1) / 2;  // slots per parity half
+    c.lstride4 = (size_t)c.NX * 16;
+    c.lstride2 = (size_t)c.NX * 8;
+    c.qstride4 = (size_t)2 * c.qhalf * 16;
+    c.qstride2 = (size_t)2 * c.qhalf * 8;
+    c.pstride = (size_t)c.NX * c.PP * 4;
+    c.off_l4 = 0;
+    c.off_q4 = c.off_l4 + 2 * c.lstride4;
+    c.off_l2 = c.off_q4 + 2 * c.qstride4;
+    c.off_q2 = c.off_l2 + 2 * c.lstride2;
+    c.off_pix = ((c.off_q2 + 2 * c.qstride2) + 15) & ~(size_t)15;
+    c.bytes = c.off_pix + 2 * c.pstride;
+    return c;
+}
+
+// broadcast form of one channel dword (bytes v, lo, hi): {v|v<<16, lo|lo<<16, hi|hi<<16}
+__device__ __forceinline__ uint3 bt_bcast(uint32_t w)
+{
+    return make_uint3(__builtin_amdgcn_perm(w, w, 0x0c040c00u), __builtin_amdgcn_perm(w, w, 0x0c050c01u),
+                      __builtin_amdgcn_perm(w, w, 0x0c060c02u));
+}
+// pair form of one channel: low halves from column a (disparity d), high from b (d+1)
+__device__ __forceinline__ uint3 bt_pairform(uint32_t a, uint32_t b)
+{
+    return make_uint3(__builtin_amdgcn_perm(b, a, 0x0c040c00u), __builtin_amdgcn_perm(b, a, 0x0c050c01u),
+                      __builtin_amdgcn_perm(b, a, 0x0c060c02u));
+}
+__device__ __forceinline__ uint32_t bt_cost2(uint4 u4, uint2 u2, uint4 v4, uint2 v2)
+{
+    const uint32_t ca = bt_pair(u4.x, u4.y, u4.z, v4.x, v4.y, v4.z);
+    const uint32_t cb = bt_pair(u4.w, u2.x, u2.y, v4.w, v2.x, v2.y);
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 two = {2, 2};
+    return pk_add_u16(ca, __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, cb) >> two));
+}
+
+template <int NR, int STG>
+__global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4))) void sgbm_cost2_kernel(const uint64_t* __restrict__ pre,
+                                                                   int W, int H, SgbmEff e, int TY,
+                                                                   int16_t* __restrict__ C)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int SH2 = NR / 2;
+    const int D = e.D, W1 = e.W1, SW2 = e.SW2;
+    const Cost2Layout lay = cost2_layout(D, SW2, TY);
+    const int PP = lay.PP, CL = lay.CL, TX = lay.TX, NX = lay.NX;
+    const int f = blockIdx.z;
+    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+    const int y1 = min(y0 + TY, H);
+    const int xclo = max(x0 - SW2, 0), xchi = min(x0 + TX + SW2 - 1, W1 - 1);
+    const int nL = xchi - xclo + 1;
+    const int nQ = nL + D - 1;
+    const int ilo = e.minX1 + xclo;
+    const int rtop = e.minX1 + xchi - e.minD;  // right column of reversed item j = 0
+    const size_t plane = (size_t)W * H;
+    const uint64_t* PL = pre + (size_t)f * 2 * plane;
+    const uint64_t* PR = PL + plane;
+    const int tid = threadIdx.x;
+    const int cl = tid / PP, p = tid - cl * PP;
+    const bool worker = cl < CL;
+    const int tx0 = cl * kCost2Run;
+    const uint32_t p2x2 = (uint32_t)(e.P2 & 0xffff) * 0x10001u;
+    const int nItems = nL + nQ;
+    // no clamped columns in this tile and an even column-lane count
+    const bool linear = x0 - SW2 >= 0 && x0 + TX + SW2 <= W1 && (CL & 1) == 0;
+
+    // staging: item i < nL -> left column ilo + i; else right pair j = i - nL
+    // (reversed columns rtop - j and rtop - j - 1, zero outside the image)
+    uint64_t pa[STG], pb[STG];
+    auto fetch_row = [&](int v) {
+        const int r = clampi(v, 0, H - 1);
+        const uint64_t* lrow = PL + (size_t)r * W;
+        const uint64_t* rrow = PR + (size_t)r * W;
+#pragma unroll
+        for (int k = 0; k < STG; k++) {
+            const int i = kCost2Threads - 1 - tid + kCost2Threads * k;  // high waves: fewer pix columns
+            const bool left = i < nL;
+            const int xa = left ? ilo + i : rtop - (i - nL);
+            const int xb = xa - 1;
+            const uint64_t* row = left ? lrow : rrow;
+            const bool oka = i < nItems && xa >= 0 && xa < W;
+            const bool okb = !left && i < nItems && xb >= 0 && xb < W;
+            const uint64_t va = row[clampi(xa, 0, W - 1)];
+            const uint64_t vb = row[clampi(xb, 0, W - 1)];
+            pa[k] = oka ? va : 0ull;
+            pb[k] = okb ? vb : 0ull;
+        }
+    };
+    auto stage_row = [&](int buf) {
+        uint4* l4 = (uint4*)(smem + lay.off_l4 + buf * lay.lstride4);
+        uint2* l2 = (uint2*)(smem + lay.off_l2 + buf * lay.lstride2);
+        uint4* q4 = (uint4*)(smem + lay.off_q4 + buf * lay.qstride4);
+        uint2* q2 = (uint2*)(smem + lay.off_q2 + buf * lay.qstride2);
+#pragma unroll
+        for (int k = 0; k < STG; k++) {
+            const int i = kCost2Threads - 1 - tid + kCost2Threads * k;  // high waves: fewer pix columns
+            if (i < nL) {
+                const uint3 fa = bt_bcast((uint32_t)pa[k]), fb = bt_bcast((uint32_t)(pa[k] >> 32));
+                l4[i] = make_uint4(fa.x, fa.y, fa.z, fb.x);
+                l2[i] = make_uint2(fb.y, fb.z);
+            } else if (i < nItems) {
+                const int j = i - nL;
+                const int q = (j & 1) * lay.qhalf + (j >> 1);
+                const uint3 fa = bt_pairform((uint32_t)pa[k], (uint32_t)pb[k]);
+                const uint3 fb = bt_pairform((uint32_t)(pa[k] >> 32), (uint32_t)(pb[k] >> 32));
+                q4[q] = make_uint4(fa.x, fa.y, fa.z, fb.x);
+                q2[q] = make_uint2(fb.y, fb.z);
+            }
+        }
+    };
+    auto pix_row = [&](int buf) {
+        const uint4* l4 = (const uint4*)(smem + lay.off_l4 + buf * lay.lstride4);
+        const uint2* l2 = (const uint2*)(smem + lay.off_l2 + buf * lay.lstride2);
+        const uint4* q4 = (const uint4*)(smem + lay.off_q4 + buf * lay.qstride4);
+        const uint2* q2 = (const uint2*)(smem + lay.off_q2 + buf * lay.qstride2);
+        uint32_t* pix = (uint32_t*)(smem + lay.off_pix + buf * lay.pstride);
+        if (!worker) return;
+        // slot of right pair j = t + 2p (t = xchi - xc)
+        auto qslot = [&](int t) { return (t & 1) * lay.qhalf + (t >> 1) + p; };
+        if (linear) {
+            // interior tile, CL even: column xv reads left slot xv and right
+            // slots qslot(nL - 1 - xv), which step by -CL/2 per iteration
+            const int t0 = nL - 1 - cl;
+            const int qs = qslot(t0), dq = CL >> 1;
+            const uint4* pl4 = l4 + cl;
+            const uint2* pl2 = l2 + cl;
+            const uint4* pq4 = q4 + qs;
+            const uint2* pq2 = q2 + qs;
+            uint32_t* pp = pix + cl * PP + p;
+#pragma unroll 1
+            for (int xv = cl; xv < NX; xv += CL) {
+                *pp = bt_cost2(*pl4, *pl2, *pq4, *pq2);
+                pl4 += CL;
+                pl2 += CL;
+                pq4 -= dq;
+                pq2 -= dq;
+                pp += CL * PP;
+            }
+            return;
+        }
+#pragma unroll 1
+        for (int xv = cl; xv < NX; xv += CL) {
+            const int xc0 = clampi(x0 - SW2 + xv, 0, W1 - 1) - xclo;
+            const int j0 = qslot(nL - 1 - xc0);
+            pix[xv * PP + p] = bt_cost2(l4[xc0], l2[xc0], q4[j0], q2[j0]);
+        }
+    };
+
+    uint32_t csum[kCost2Run], ring[NR][kCost2Run];
+#pragma unroll
+    for (int i = 0; i < kCost2Run; i++) {
+        csum[i] = 0;
+#pragma unroll
+        for (int s = 0; s < NR; s++) ring[s][i] = 0;
+    }
+
+    const int vstart = y0 - SH2;
+    const int nrows = (y1 - y0) + 2 * SH2;
+    // row k of the sweep emits cost row y = y0 - 2*SH2 + k (once k >= NR - 1)
+    const size_t ostride = (size_t)W1 * PP;  // dwords per cost row
+    uint32_t* obase = (uint32_t*)C + (((size_t)f * H + y0) * W1 + x0 + tx0) * PP + p -
+                      (size_t)(2 * SH2) * ostride;
+    const int nout = min(kCost2Run, W1 - (x0 + tx0));
+    fetch_row(vstart);
+    stage_row(0);
+    if (nrows > 1) fetch_row(vstart + 1);
+    __syncthreads();
+    for (int base = 0; base < nrows; base += NR) {
+#pragma unroll
+        for (int s = 0; s < NR; s++) {
+            const int k = base + s;
+            if (k >= nrows) break;
+            const int buf = k & 1;
+            if (k + 1 < nrows) {
+                stage_row(buf ^ 1);
+                if (k + 2 < nrows) fetch_row(vstart + k + 2);
+            }
+            pix_row(buf);
+            __syncthreads();  // pix[buf] complete; staging of row k+1 visible
+            if (worker) {
+                const uint32_t* pr =
+                    (const uint32_t*)(smem + lay.off_pix + buf * lay.pstride) + tx0 * PP + p;
+                uint32_t h = 0;
+                for (int q = 0; q <= 2 * SW2; q++) h = pk_add_u16(h, pr[q * PP]);
+                const bool emit = k >= NR - 1;
+                uint32_t* orow = obase + (size_t)k * ostride;
+#pragma unroll
+                for (int i = 0; i < kCost2Run; i++) {
+                    if (i > 0)
+                        h = pk_sub_u16(pk_add_u16(h, pr[(i + 2 * SW2) * PP]), pr[(i - 1) * PP]);
+                    csum[i] = pk_add_u16(pk_sub_u16(csum[i], ring[s][i]), h);
+                    ring[s][i] = h;
+                    if (emit && i < nout) orow[i * PP] = pk_add_u16(p2x2, csum[i]);
+                }
+            }
+        }
+    }
+}
+
 // 3. OpenCV 3.4 cost-row quirks (see oracle/twin.py sgbm_cost_volume):
 //    rows y >= 1 never refresh column x = 0; rows with y + SH2 >= H are never
 //    recomputed (MODE_SGBM keeps the last computed row, MODE_HH keeps P2).
@@ -830,6 +1067,13 @@ __global__ __launch_bounds__(64) void sgbm_final16_kernel(const int16_t* __restr
         cb[j].load(cp - t * D);
         AV::load(sp - t * D, sb[j]);
     }
+    // Per step the row's 16 lanes agree on K = (minS << 16 | lane-rule sub),
+    // S[best-1], S[best+1] and the uniqueness verdict; lane (s & 15) keeps them,
+    // and every 16 steps the 16 lanes finish 16 columns at once (sub-pixel
+    // division, raw store, right-view atomicMin) -- the per-step path stays
+    // branch-free so consecutive steps overlap.
+    uint32_t kK = 0xffffffffu, kS = 0;  // kept: K, (Sp << 16 | Sm & 0xffff)
+    int kRej = 0;
     auto body = [&](int s, int j) {
         const int dl = (int16_t)(minp + e.P2);
         const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
@@ -865,8 +1109,7 @@ __global__ __launch_bounds__(64) void sgbm_final16_kernel(const int16_t* __restr
         const int K = row_min_i32(key);
         const int minS = K >> 16;
         const int sub = K & 0xffff;
-        int best = lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
-        if (minS >= kMaxCost) best = -1;  // no strict minimum below MAX_COST
+        const int best = lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
         int rej = 0;
         if (uq != 0) {  // with uq == 0 the test reads S[d] < minS: never true
 #pragma unroll
@@ -878,8 +1121,8 @@ __global__ __launch_bounds__(64) void sgbm_final16_kernel(const int16_t* __restr
                     rej |= (v * (100 - uq) < minS * 100) && (abs(best - d) > 1);
                 }
             }
+            rej = row_max_i32(rej);
         }
-        rej = row_max_i32(rej);
         // S[best-1], S[best+1] from the owning lanes of the row
         auto fetch = [&](int d) -> int {
             d = clampi(d, 0, D - 1);
@@ -891,35 +1134,55 @@ __global__ __launch_bounds__(64) void sgbm_final16_kernel(const int16_t* __restr
             return (el & 1) ? hi16(w) : lo16(w);
         };
         const int Sm = fetch(best - 1), Sp = fetch(best + 1);
-        if (rl == 0 && exists && !rej) {
-            const int x = W1 - 1 - s;
-            int d16;
-            if (0 < best && best < D - 1) {
-                const int den = max(Sm + Sp - 2 * minS, 1);
-                d16 = best * kDispScale + ((Sm - Sp) * kDispScale + den) / (den * 2);
-            } else {
-                d16 = best * kDispScale;
-            }
-            orow[x + minX1] = (int16_t)(d16 + minD * kDispScale);
-            const int x2 = x + minX1 - best - minD;
-            if (minS < kMaxCost && x2 >= 0 && x2 < W)
-                atomicMin(krow + x2, ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
+        const bool mine = rl == (s & 15);
+        kK = mine ? (uint32_t)K : kK;
+        kS = mine ? (((uint32_t)Sp << 16) | ((uint32_t)Sm & 0xffffu)) : kS;
+        kRej = mine ? rej : kRej;
+    };
+    // lane rl finishes column s0 + rl of the sweep (x = W1 - 1 - s)
+    auto flush = [&](int s0, int cnt) {
+        const int s = s0 + rl;
+        if (!exists || rl >= cnt || kRej) return;
+        const int minS = (int)(kK >> 16);
+        const int sub = (int)(kK & 0xffffu);
+        int best = lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
+        if (minS >= kMaxCost) best = -1;  // no strict minimum below MAX_COST
+        const int Sm = (int)(int16_t)(kS & 0xffffu), Sp = (int)(int16_t)(kS >> 16);
+        const int x = W1 - 1 - s;
+        int d16;
+        if (0 < best && best < D - 1) {
+            const int den = max(Sm + Sp - 2 * minS, 1);
+            d16 = best * kDispScale + ((Sm - Sp) * kDispScale + den) / (den * 2);
+        } else {
+            d16 = best * kDispScale;
         }
+        orow[x + minX1] = (int16_t)(d16 + minD * kDispScale);
+        const int x2 = x + minX1 - best - minD;
+        if (minS < kMaxCost && x2 >= 0 && x2 < W)
+            atomicMin(krow + x2, ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
     };
     int s = 0;
-    for (; s + PF <= W1; s += PF) {
+    for (; s + 16 <= W1; s += 16) {
 #pragma unroll
-        for (int j = 0; j < PF; j++) {
-            body(s + j, j);
+        for (int j = 0; j < 16; j++) {
+            body(s + j, j % PF);
             const ptrdiff_t t = min(s + j + PF, W1 - 1);
-            cb[j].load(cp - t * D);
-            AV::load(sp - t * D, sb[j]);
+            cb[j % PF].load(cp - t * D);
+            AV::load(sp - t * D, sb[j % PF]);
         }
+        flush(s, 16);
     }
     const int rem = W1 - s;
 #pragma unroll
-    for (int j = 0; j < PF; j++)
-        if (j < rem) body(s + j, j);
+    for (int j = 0; j < 16; j++) {
+        if (j < rem) {
+            body(s + j, j % PF);
+            const ptrdiff_t t = min(s + j + PF, W1 - 1);
+            cb[j % PF].load(cp - t * D);
+            AV::load(sp - t * D, sb[j % PF]);
+        }
+    }
+    if (rem > 0) flush(s, rem);
     __threadfence_block();
     __syncthreads();
     if (!exists) return;
@@ -1217,6 +1480,77 @@ int launch_paths_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
 
 }  // namespace
 
+// Cost-volume launch: the register-ring kernel when blockSize <= 15 and the
+// tile fits, else the LDS-ring kernel.
+static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int TY,
+                       const uint64_t* pre, int16_t* Cv)
+{
+    hipStream_t s = ctx->stream;
+    int rc;
+    if (ctx->cost2 && e.SH2 <= 7) {
+        const Cost2Layout l2 = cost2_layout(e.D, e.SW2, TY);
+        const int items = 2 * l2.NX + e.D - 1;
+        if (l2.CL >= 1 && items <= kCost2Threads * 2 &&
+            l2.bytes <= 160 * 1024) {
+            dim3 grid2((e.W1 + l2.TX - 1) / l2.TX, (H + TY - 1) / TY, n);
+            void (*kern)(const uint64_t*, int, int, SgbmEff, int, int16_t*) = nullptr;
+            const bool two = items > kCost2Threads;
+            if (!two) {
+                switch (2 * e.SH2 + 1) {
+                case 1: kern = sgbm_cost2_kernel<1, 1>; break;
+                case 3: kern = sgbm_cost2_kernel<3, 1>; break;
+                case 5: kern = sgbm_cost2_kernel<5, 1>; break;
+                case 7: kern = sgbm_cost2_kernel<7, 1>; break;
+                case 9: kern = sgbm_cost2_kernel<9, 1>; break;
+                case 11: kern = sgbm_cost2_kernel<11, 1>; break;
+                case 13: kern = sgbm_cost2_kernel<13, 1>; break;
+                default: kern = sgbm_cost2_kernel<15, 1>; break;
+                }
+            } else {
+                switch (2 * e.SH2 + 1) {
+                case 1: kern = sgbm_cost2_kernel<1, 2>; break;
+                case 3: kern = sgbm_cost2_kernel<3, 2>; break;
+                case 5: kern = sgbm_cost2_kernel<5, 2>; break;
+                case 7: kern = sgbm_cost2_kernel<7, 2>; break;
+                case 9: kern = sgbm_cost2_kernel<9, 2>; break;
+                case 11: kern = sgbm_cost2_kernel<11, 2>; break;
+                case 13: kern = sgbm_cost2_kernel<13, 2>; break;
+                default: kern = sgbm_cost2_kernel<15, 2>; break;
+                }
+            }
+            if (l2.bytes > 65536 &&
+                (rc = check_hip(ctx, hipFuncSetAttribute((const void*)kern,
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                         (int)l2.bytes),
+                                "sgbm cost LDS attribute")))
+                return rc;
+            {
+                StageTimer tm(ctx, kStageCost);
+                hipLaunchKernelGGL(kern, grid2, dim3(kCost2Threads), l2.bytes, s, pre, W, H, e, TY,
+                                   Cv);
+            }
+            return check_hip(ctx, hipGetLastError(), "sgbm cost kernel");
+        }
+    }
+    CostLayout lay = cost_layout(e.D, e.SW2, e.SH2, TY);
+    if (lay.nLmax + lay.nRmax + 1 > 256 * kStageRegs)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "numDisparities too large for the GPU cost kernel");
+    if (lay.bytes > 160 * 1024)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "blockSize too large for the GPU cost kernel");
+    dim3 cgrid((e.W1 + lay.TX - 1) / lay.TX, (H + TY - 1) / TY, n);
+    if (lay.bytes > 65536 &&
+        (rc = check_hip(ctx, hipFuncSetAttribute((const void*)sgbm_cost_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)lay.bytes),
+                        "sgbm cost LDS attribute")))
+        return rc;
+    {
+        StageTimer tm(ctx, kStageCost);
+        hipLaunchKernelGGL(sgbm_cost_kernel, cgrid, dim3(256), lay.bytes, s, pre, W, H, e, TY, Cv);
+    }
+    return check_hip(ctx, hipGetLastError(), "sgbm cost kernel");
+}
+
 int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, const uint8_t* R,
                 size_t rs, size_t rfs, int W, int H, const SgbmEff& e, int16_t* out, size_t os,
                 size_t ofs)
@@ -1250,23 +1584,7 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
 
     // cost volume: one block per TX x TY tile; keep the LDS image <= 160 KiB
     int TY = H >= 512 ? 96 : (H >= 256 ? 48 : 16);
-    CostLayout lay = cost_layout(e.D, e.SW2, e.SH2, TY);
-    if (lay.nLmax + lay.nRmax + 1 > 256 * kStageRegs)
-        return set_error(ctx, MVSV_E_INVALID_ARG, "numDisparities too large for the GPU cost kernel");
-    if (lay.bytes > 160 * 1024)
-        return set_error(ctx, MVSV_E_INVALID_ARG, "blockSize too large for the GPU cost kernel");
-    dim3 cgrid((e.W1 + lay.TX - 1) / lay.TX, (H + TY - 1) / TY, n);
-    if (lay.bytes > 65536 &&
-        (rc = check_hip(ctx, hipFuncSetAttribute((const void*)sgbm_cost_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 (int)lay.bytes),
-                        "sgbm cost LDS attribute")))
-        return rc;
-    {
-        StageTimer tm(ctx, kStageCost);
-        hipLaunchKernelGGL(sgbm_cost_kernel, cgrid, dim3(256), lay.bytes, s, pre, W, H, e, TY, Cv);
-    }
-    if ((rc = check_hip(ctx, hipGetLastError(), "sgbm cost kernel"))) return rc;
+    if ((rc = launch_cost(ctx, n, W, H, e, TY, pre, Cv))) return rc;
 
     const int ybot = std::max(H - e.SH2, 1);     // first row that is never recomputed
     const int ylast = std::max(H - e.SH2 - 1, 0);  // last recomputed row

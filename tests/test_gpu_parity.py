@@ -97,6 +97,26 @@ def test_sgbm_synthetic_modes(gpu, mvsv, oracle, mode, D):
     assert np.array_equal(got, want), report(got, want)
 
 
+@pytest.mark.parametrize("bs", [13, 15, 17, 21])
+@pytest.mark.parametrize("D", [64, 128])
+def test_sgbm_block_sizes(gpu, mvsv, oracle, bs, D):
+    # blockSize <= 15: register-ring cost kernel; larger: the LDS-ring kernel
+    L, R = mvsv.synth_pair(SEED0 + bs, 360, 80, 0, D)
+    got, want = sgbm_both(mvsv, oracle, L, R, minDisparity=1, numDisparities=D, blockSize=bs,
+                          uniquenessRatio=10, speckleWindowSize=30, speckleRange=2, mode=bs & 1 ^ 1)
+    assert np.array_equal(got, want), report(got, want)
+
+
+@pytest.mark.parametrize("D", [16, 512])
+def test_sgbm_staging_two_slots(gpu, mvsv, oracle, D):
+    # shapes whose cost-kernel staging needs two items per thread
+    W = 700 if D == 512 else 600
+    L, R = mvsv.synth_pair(SEED0 + 7 * D, W, 40, 0, D)
+    got, want = sgbm_both(mvsv, oracle, L, R, minDisparity=-3, numDisparities=D, blockSize=7,
+                          P1=200, P2=800, mode=1)
+    assert np.array_equal(got, want), report(got, want)
+
+
 def test_sgbm_all_invalid_when_no_columns(gpu, mvsv, oracle):
     L, R = mvsv.synth_pair(SEED0, 40, 20, 0, 64)
     got, want = sgbm_both(mvsv, oracle, L, R, minDisparity=0, numDisparities=64, blockSize=5)
