@@ -280,6 +280,7 @@ int mvsv_trim(mvsv_ctx* ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     DevBuf* all[] = {&ctx->pre, &ctx->cost, &ctx->agg, &ctx->raw, &ctx->uf_parent, &ctx->uf_size,
+                     &ctx->uf_tile,
                      &ctx->dummy, &ctx->keys,
                      &ctx->bm_lf, &ctx->bm_rf, &ctx->bm_cost, &ctx->h_left, &ctx->h_right,
                      &ctx->h_out};

@@ -60,7 +60,7 @@ struct mvsv_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // SGBM
-    mvsv::DevBuf pre, cost, agg, raw, uf_parent, uf_size, dummy, keys;
+    mvsv::DevBuf pre, cost, agg, raw, uf_parent, uf_size, uf_tile, dummy, keys;
     int path16 = 1;  // 16-lanes-per-scanline path kernels where D allows
     int cost2 = 1;   // register-ring cost kernel where blockSize <= 15
     // BM

@@ -55,50 +55,11 @@ __global__ __launch_bounds__(256) void median3x3_kernel(const int16_t* __restric
 }
 
 // ---- speckle filter: union-find ----------------------------------------------
-// Lock-free union-find in the style of ECL-CC: roots are linked towards the
-// smaller index with atomicMin (parent pointers only ever decrease and always
-// stay inside their component), find() halves paths with atomicMin as well, so
-// concurrent unions can never lose a link.  Parent words are read with
-// agent-scope relaxed atomics (L1-bypassing): other workgroups rewrite them
-// inside the same launch.
-__device__ __forceinline__ int uf_load(const int* p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ int uf_find(int* parent, int i)
-{
-    int p = uf_load(parent + i);
-    while (p != i) {
-        int gp = uf_load(parent + p);
-        if (gp != p) atomicMin(parent + i, gp);  // path halving, never increases
-        i = p;
-        p = gp;
-    }
-    return i;
-}
-
-__device__ void uf_unite(int* parent, int a, int b)
-{
-    for (;;) {
-        a = uf_find(parent, a);
-        b = uf_find(parent, b);
-        if (a == b) return;
-        if (a > b) {
-            int t = a;
-            a = b;
-            b = t;
-        }
-        int old = atomicMin(parent + b, a);  // link root b under a (a < b)
-        if (old == b) return;
-        b = old;  // b was re-linked concurrently: continue with its new parent
-    }
-}
-
 // Stage 1: union-find inside a 32x32 tile in LDS (one 256-thread block per
-// tile, 4 pixels per thread), then every pixel's global parent = its tile-local
-// root (row-major local order is monotone in the global index, so roots stay
-// the smallest index of their tile component).  Also zeroes the size array.
+// tile, 4 pixels per thread).  Every valid pixel's global parent = its
+// tile-local root (row-major local order is monotone in the global index, so
+// roots stay the smallest index of their tile component); tile[root] = the
+// tile component's pixel count, tile[other] = 0; size[root] = 0.
 constexpr int kSpTile = 32;
 
 __device__ __forceinline__ int lds_load(const int* p)
@@ -139,11 +100,14 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(const int16_t* __res
                                                             size_t st, size_t fs, int W, int H,
                                                             int new_val, int max_diff,
                                                             int* __restrict__ parent,
+                                                            int* __restrict__ tile,
                                                             int* __restrict__ size)
 {
     __shared__ int lpar[kSpTile * kSpTile];
     __shared__ int lval[kSpTile * kSpTile];
+    __shared__ int lcnt[kSpTile * kSpTile];
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    const int lane = threadIdx.x & 63;
     const int x0 = blockIdx.x * kSpTile, y0 = blockIdx.y * kSpTile;
     const int f = blockIdx.z;
     const int16_t* s = img + f * fs;
@@ -159,6 +123,7 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(const int16_t* __res
         }
         lval[li] = v;
         lpar[li] = li;
+        lcnt[li] = 0;
     }
     __syncthreads();
 #pragma unroll
@@ -176,7 +141,26 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(const int16_t* __res
         }
     }
     __syncthreads();
+    int root[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int ly = ty + 8 * k, li = ly * kSpTile + tx;
+        root[k] = lval[li] != kInvalid ? lfind(lpar, li) : -1;
+        // wave-aggregated count: lanes sharing a root add once
+        bool pending = root[k] >= 0;
+        for (;;) {
+            unsigned long long m = __ballot(pending);
+            if (m == 0ull) break;
+            const int leader = __ffsll((long long)m) - 1;
+            const int r0 = __builtin_amdgcn_readlane(root[k], leader);
+            const unsigned long long same = __ballot(pending && root[k] == r0);
+            if (lane == leader) atomicAdd(lcnt + r0, __popcll(same));
+            if (root[k] == r0) pending = false;
+        }
+    }
+    __syncthreads();
     int* par = parent + (size_t)f * W * H;
+    int* tl = tile + (size_t)f * W * H;
     int* sz = size + (size_t)f * W * H;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -184,17 +168,58 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(const int16_t* __res
         const int gx = x0 + tx, gy = y0 + ly;
         if (gx >= W || gy >= H) continue;
         const int gi = gy * W + gx;
-        int g = gi;
-        if (lval[li] != kInvalid) {
-            const int r = lfind(lpar, li);
-            g = (y0 + r / kSpTile) * W + x0 + (r % kSpTile);
-        }
-        par[gi] = g;
-        sz[gi] = 0;
+        const int r = root[k];
+        par[gi] = r >= 0 ? (y0 + r / kSpTile) * W + x0 + (r % kSpTile) : gi;
+        const int c = lcnt[li];
+        tl[gi] = c;
+        if (c > 0) sz[gi] = 0;
     }
 }
 
-// Stage 2: unions across tile borders only (right and bottom edge of each tile).
+// Union-find over tile components (the global parent words of tile roots).
+// Parent words are read with agent-scope relaxed atomics (L1-bypassing):
+// other workgroups rewrite them inside the same launch.  Roots are linked
+// towards the smaller index with atomicMin (ECL-CC style): parents only ever
+// decrease and stay inside their component, so concurrent unions never lose a
+// link.
+__device__ __forceinline__ int uf_load(const int* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ int uf_find(int* parent, int i)
+{
+    int p = uf_load(parent + i);
+    while (p != i) {
+        int gp = uf_load(parent + p);
+        if (gp != p) atomicMin(parent + i, gp);  // path halving, never increases
+        i = p;
+        p = gp;
+    }
+    return i;
+}
+
+__device__ void uf_unite(int* parent, int a, int b)
+{
+    for (;;) {
+        a = uf_find(parent, a);
+        b = uf_find(parent, b);
+        if (a == b) return;
+        if (a > b) {
+            int t = a;
+            a = b;
+            b = t;
+        }
+        int old = atomicMin(parent + b, a);  // link root b under a (a < b)
+        if (old == b) return;
+        b = old;  // b was re-linked concurrently: continue with its new parent
+    }
+}
+
+// Stage 2: unions across tile borders (right and bottom edge of each tile),
+// one wave per tile.  A pair joins the two pixels' tile components; lanes
+// whose (component, component) pair repeats a lower lane's skip it, so a
+// tile edge inside one smooth region costs one union instead of 32.
 __global__ __launch_bounds__(64) void speckle_border_kernel(const int16_t* __restrict__ img,
                                                             size_t st, size_t fs, int W, int H,
                                                             int new_val, int max_diff,
@@ -215,52 +240,52 @@ __global__ __launch_bounds__(64) void speckle_border_kernel(const int16_t* __res
         nx = x;
         ny = y + 1;
     }
-    if (x >= W || y >= H || nx >= W || ny >= H) return;
-    const int16_t* s = img + f * fs;
-    const int v = s[(size_t)y * st + x], u = s[(size_t)ny * st + nx];
-    if (v == new_val || u == new_val || abs(v - u) > max_diff) return;
-    uf_unite(parent + (size_t)f * W * H, y * W + x, ny * W + nx);
-}
-
-// Flatten every valid pixel onto its root and count component sizes.  Lanes
-// of a wave that share a root add once (ballot aggregation); a root whose
-// count already exceeds max_size is no longer incremented -- only
-// "size <= max_size" is ever tested, and a skip needs max_size + 1 prior adds.
-__global__ __launch_bounds__(256) void speckle_count_kernel(const int16_t* __restrict__ img,
-                                                            size_t st, size_t fs, int W, int H,
-                                                            int new_val, int max_size,
-                                                            int* __restrict__ parent,
-                                                            int* __restrict__ size)
-{
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const int f = blockIdx.z;
-    const int lane = threadIdx.x & 63;
     int* par = parent + (size_t)f * W * H;
-    int* sz = size + (size_t)f * W * H;
-    int r = -1;
-    if (x < W && y < H && img[f * fs + (size_t)y * st + x] != new_val) {
-        const int i = y * W + x;
-        r = uf_find(par, i);
-        par[i] = r;
+    int a = -1, b = -1;
+    if (x < W && y < H && nx < W && ny < H) {
+        const int16_t* s = img + f * fs;
+        const int v = s[(size_t)y * st + x], u = s[(size_t)ny * st + nx];
+        if (v != new_val && u != new_val && abs(v - u) <= max_diff) {
+            a = par[y * W + x];  // tile roots (written by stage 1)
+            b = par[ny * W + nx];
+        }
     }
-    bool pending = r >= 0;
+    bool pending = a >= 0;
     for (;;) {
         unsigned long long m = __ballot(pending);
         if (m == 0ull) break;
         const int leader = __ffsll((long long)m) - 1;
-        const int r0 = __builtin_amdgcn_readlane(r, leader);
-        const unsigned long long same = __ballot(pending && r == r0);
-        if (lane == leader && uf_load(sz + r0) <= max_size)
-            atomicAdd(sz + r0, __popcll(same));
-        if (r == r0) pending = false;
+        const int a0 = __builtin_amdgcn_readlane(a, leader);
+        const int b0 = __builtin_amdgcn_readlane(b, leader);
+        if (t == leader) uf_unite(par, a0, b0);
+        if (a == a0 && b == b0) pending = false;
     }
 }
 
+// Stage 3: per tile component: its global root, the component sizes, and the
+// tile word becomes ~root (negative: "resolved").
+__global__ __launch_bounds__(256) void speckle_count_kernel(int W, int H, int* __restrict__ parent,
+                                                            int* __restrict__ tile,
+                                                            int* __restrict__ size)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int f = blockIdx.y;
+    if (i >= W * H) return;
+    int* tl = tile + (size_t)f * W * H;
+    const int c = tl[i];
+    if (c <= 0) return;
+    int* par = parent + (size_t)f * W * H;
+    const int g = uf_find(par, i);
+    atomicAdd(size + (size_t)f * W * H + g, c);
+    tl[i] = ~g;
+}
+
+// Stage 4: pixel -> tile root -> global root -> size.
 __global__ __launch_bounds__(256) void speckle_apply_kernel(int16_t* __restrict__ img, size_t st,
                                                             size_t fs, int W, int H, int new_val,
                                                             int max_size,
                                                             const int* __restrict__ parent,
+                                                            const int* __restrict__ tile,
                                                             const int* __restrict__ size)
 {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -270,8 +295,11 @@ __global__ __launch_bounds__(256) void speckle_apply_kernel(int16_t* __restrict_
     int16_t* p = img + f * fs + (size_t)y * st + x;
     if (*p == new_val) return;
     const size_t base = (size_t)f * W * H;
-    const int r = parent[base + y * W + x];
-    if (size[base + r] <= max_size) *p = (int16_t)new_val;
+    const int i = y * W + x;
+    int t = tile[base + i];
+    if (t >= 0) t = tile[base + parent[base + i]];  // not a tile root: its root's word
+    const int g = ~t;
+    if (size[base + g] <= max_size) *p = (int16_t)new_val;
 }
 
 // ---- MeanDisparityDetection::build(MEAN_VALUE) --------------------------------
@@ -329,19 +357,22 @@ int speckle_device(mvsv_ctx* ctx, int n, int16_t* img, size_t st, size_t fs, int
     const size_t npix = (size_t)W * H;
     if ((rc = ensure(ctx, ctx->uf_parent, (size_t)n * npix * 4, "speckle labels"))) return rc;
     if ((rc = ensure(ctx, ctx->uf_size, (size_t)n * npix * 4, "speckle sizes"))) return rc;
+    if ((rc = ensure(ctx, ctx->uf_tile, (size_t)n * npix * 4, "speckle tile components")))
+        return rc;
     int* parent = (int*)ctx->uf_parent.ptr;
     int* size = (int*)ctx->uf_size.ptr;
+    int* tile = (int*)ctx->uf_tile.ptr;
     hipStream_t s = ctx->stream;
     dim3 tiles((W + kSpTile - 1) / kSpTile, (H + kSpTile - 1) / kSpTile, n);
     hipLaunchKernelGGL(speckle_local_kernel, tiles, dim3(256), 0, s, img, st, fs, W, H, new_val,
-                       max_diff, parent, size);
+                       max_diff, parent, tile, size);
     hipLaunchKernelGGL(speckle_border_kernel, tiles, dim3(64), 0, s, img, st, fs, W, H, new_val,
                        max_diff, parent);
+    hipLaunchKernelGGL(speckle_count_kernel, dim3((unsigned)((npix + 255) / 256), n), dim3(256), 0,
+                       s, W, H, parent, tile, size);
     dim3 grid((W + 63) / 64, (H + 3) / 4, n);
-    hipLaunchKernelGGL(speckle_count_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val,
-                       max_size, parent, size);
     hipLaunchKernelGGL(speckle_apply_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val,
-                       max_size, parent, size);
+                       max_size, parent, tile, size);
     return check_hip(ctx, hipGetLastError(), "speckle filter");
 }
 
