@@ -262,6 +262,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
     if (const char* v = std::getenv("MVSV_KERNELS")) {
         if (std::strstr(v, "cost-lds")) c->cost2 = 0;
         if (std::strstr(v, "path-wave")) c->path16 = 0;
+        if (std::strstr(v, "path-lines")) c->tri = 0;
     }
     *out = c;
     return MVSV_OK;
@@ -280,7 +281,7 @@ int mvsv_trim(mvsv_ctx* ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     DevBuf* all[] = {&ctx->pre, &ctx->cost, &ctx->agg, &ctx->raw, &ctx->uf_parent, &ctx->uf_size,
-                     &ctx->uf_tile,
+                     &ctx->uf_tile, &ctx->tri_bnd, &ctx->status,
                      &ctx->dummy, &ctx->keys,
                      &ctx->bm_lf, &ctx->bm_rf, &ctx->bm_cost, &ctx->h_left, &ctx->h_right,
                      &ctx->h_out};
@@ -367,11 +368,26 @@ int mvsv_use_own_stream(mvsv_ctx* ctx)
 
 void* mvsv_get_stream(mvsv_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
+// Device status word (set by a kernel that had to give up, e.g. a strip-boundary
+// wait of the sheared-strip path kernel that timed out): read after a sync.
+static int check_status(mvsv_ctx* ctx)
+{
+    if (!ctx->status.ptr) return MVSV_OK;
+    int v = 0;
+    int rc = check_hip(ctx, hipMemcpy(&v, ctx->status.ptr, sizeof(v), hipMemcpyDeviceToHost),
+                       "status read");
+    if (rc) return rc;
+    if (v == 0) return MVSV_OK;
+    (void)hipMemset(ctx->status.ptr, 0, sizeof(v));
+    return set_error(ctx, MVSV_E_HIP, "sgbm path kernel: strip-boundary wait timed out");
+}
+
 int mvsv_synchronize(mvsv_ctx* ctx)
 {
     if (!ctx) return MVSV_E_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
-    return check_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    int rc = check_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    return rc ? rc : check_status(ctx);
 }
 
 size_t mvsv_sgbm_workspace_bytes(int n, int W, int H, const mvsv_sgbm_params* p)
@@ -459,7 +475,8 @@ static int host_call(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* 
                           (const uint8_t*)ctx->h_right.ptr, W, fb, W, H, be, dout, W, fb);
     if (rc) return rc;
     if ((rc = check_hip(ctx, hipMemcpy2DAsync(out, os * 2, dout, (size_t)W * 2, (size_t)W * 2, H, hipMemcpyDeviceToHost, s), "D2H out"))) return rc;
-    return check_hip(ctx, hipStreamSynchronize(s), "hipStreamSynchronize");
+    if ((rc = check_hip(ctx, hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
+    return check_status(ctx);
 }
 
 int mvsv_sgbm(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* R, size_t rs, int W,

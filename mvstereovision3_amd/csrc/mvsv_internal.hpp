@@ -60,9 +60,11 @@ struct mvsv_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // SGBM
-    mvsv::DevBuf pre, cost, agg, raw, uf_parent, uf_size, uf_tile, dummy, keys;
+    mvsv::DevBuf pre, cost, agg, raw, uf_parent, uf_size, uf_tile, dummy, keys, tri_bnd, status;
+    unsigned tri_epoch = 0;  // tag of the strip-boundary granules of the last launch
     int path16 = 1;  // 16-lanes-per-scanline path kernels where D allows
     int cost2 = 1;   // register-ring cost kernel where blockSize <= 15
+    int tri = 1;     // sheared-strip kernels: three directions per sweep
     // BM
     mvsv::DevBuf bm_lf, bm_rf, bm_cost;
     // host-pointer staging

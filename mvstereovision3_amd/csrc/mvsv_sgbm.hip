@@ -931,7 +931,7 @@ __device__ __forceinline__ int lane_min_row(const uint32_t (&ln)[NP])
     return min(lo16(m), hi16(m));
 }
 
-constexpr int kPath16PF = 8;
+constexpr int kPath16PF = 12;
 
 template <int NP, bool FIRST, typename AccT>
 __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restrict__ C,
@@ -1006,6 +1006,310 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
 #pragma unroll
     for (int j = 0; j < PF; j++)
         if (j < rem) body(s + j, j);
+}
+
+// ---------------------------------------------------------------------------
+// 4c. three vertical-ish directions in one sweep over sheared strips.
+// With U = x - t + (H - 1) for step t (row y = t top-down, y = H-1-t
+// bottom-up), the cell (x, y) at step t has its predecessors at step t-1 in
+// U-column U (dir (1, sy)), U+1 (dir (0, sy)) and U+2 (dir (-1, sy)), sy = +1
+// (down) or -1 (up).  So one block owning U-columns [U0, U0+SW) walks its
+// strip one step per row -- every step is SW contiguous x-columns of C and of
+// the accumulator -- and needs only the two U-columns right of it from the
+// previous step: the strip to its right (lower block index) publishes them as
+// 8-byte {epoch, value} granules with write-through stores, this strip polls
+// them (bounded spin).  C and the accumulator are read once for three
+// directions instead of three times.  Cells outside the image carry L = 0,
+// min 0: exactly the zero start state of every path at the image border.
+// Lanes: 16 per U-column (2*NP disparities each), 4 columns per wave, SWW
+// waves per block; neighbours in U go through a double-buffered LDS row.
+// ---------------------------------------------------------------------------
+constexpr int kTriWaves = 8;
+constexpr int kTriSW = 4 * kTriWaves;  // U-columns per strip
+constexpr int kTriPF = 2;               // steps of C / accumulator prefetch
+constexpr unsigned kTriSpinLimit = 1u << 16;
+
+template <int NP>
+struct TriLayout {
+    static constexpr int kCols = kTriSW + 2;           // + two columns of the right strip
+    static constexpr int kColDw = 16 * NP;              // dwords per column
+    static constexpr int kBufDw = 2 * kCols * kColDw;   // dirs b and c
+    static constexpr int kLDw = 2 * kBufDw;             // double-buffered
+    static constexpr int kMinInts = 2 * 2 * kCols;      // [buf][dir][col]
+    static constexpr size_t kBytes = (size_t)(kLDw + kMinInts) * 4;
+};
+
+// Boundary granules of one strip and step: [3 items][16 lanes][NG] u64.
+// Item 0 = L of dir (0, sy) at the strip's first column, 1 = dir (-1, sy) at
+// the first column, 2 = dir (-1, sy) at the second column.  A lane's item is
+// its 2*NP int16 costs + the column min, three int16 per granule under a
+// 16-bit launch tag (bits 48-63): the tag is the data-ready flag.
+template <int NP>
+struct TriGran {
+    static constexpr int NG = (2 * NP + 1 + 2) / 3;
+    static __device__ __forceinline__ void pack(const uint32_t (&v)[NP], int mn, unsigned long long tag,
+                                                unsigned long long (&g)[NG])
+    {
+        uint32_t s[3 * NG];
+#pragma unroll
+        for (int i = 0; i < 3 * NG; i++) s[i] = 0u;
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            s[2 * p] = v[p] & 0xffffu;
+            s[2 * p + 1] = v[p] >> 16;
+        }
+        s[2 * NP] = (uint32_t)mn & 0xffffu;
+#pragma unroll
+        for (int i = 0; i < NG; i++)
+            g[i] = tag | ((unsigned long long)s[3 * i + 2] << 32) | (s[3 * i + 1] << 16) | s[3 * i];
+    }
+    static __device__ __forceinline__ void unpack(const unsigned long long (&g)[NG], uint32_t (&v)[NP],
+                                                  int& mn)
+    {
+        uint32_t s[3 * NG];
+#pragma unroll
+        for (int i = 0; i < NG; i++) {
+            s[3 * i] = (uint32_t)g[i] & 0xffffu;
+            s[3 * i + 1] = (uint32_t)g[i] >> 16;
+            s[3 * i + 2] = (uint32_t)(g[i] >> 32) & 0xffffu;
+        }
+#pragma unroll
+        for (int p = 0; p < NP; p++) v[p] = s[2 * p] | (s[2 * p + 1] << 16);
+        mn = (int)(int16_t)s[2 * NP];
+    }
+};
+
+template <int NP>
+__device__ __forceinline__ size_t tri_slot(int f, int k, int t, int nframes, int H)
+{
+    return ((((size_t)k * nframes + f) * H + t) * 3) * 16 * TriGran<NP>::NG;
+}
+
+template <int NP, bool FIRST, typename AccT>
+__global__ __launch_bounds__(64 * kTriWaves) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
+    const int16_t* __restrict__ C, AccT* __restrict__ A, AccT* __restrict__ dummy, int H, int W1,
+    int D, int sy, int P1, int P2, unsigned long long* __restrict__ bnd, unsigned epoch,
+    int nframes, int nstrips, int* __restrict__ status)
+{
+    using AV = AccVec<NP, AccT>;
+    using TL = TriLayout<NP>;
+    using TG = TriGran<NP>;
+    constexpr int NG = TG::NG;
+    constexpr int PF = kTriPF;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* lds = (uint32_t*)smem;
+    int* lmin = (int*)(lds + TL::kLDw);
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane >> 4, rl = lane & 15;
+    // strips counted from the right, frames interleaved: every block's
+    // producer (same frame, strip k-1) has a lower block index
+    const int k = blockIdx.x / nframes;
+    const int f = blockIdx.x - k * nframes;
+    const int Utot = W1 + H - 1;
+    const int U0 = Utot - kTriSW * (k + 1);
+    const int col = 4 * w + r;
+    const int U = U0 + col;
+    // active steps: some column of the strip has 0 <= x = U - (H-1) + t < W1
+    const int tb = max(0, (H - 1) - (U0 + kTriSW - 1));
+    const int te = min(H, W1 + (H - 1) - U0);
+    if (tb >= te) return;
+    const int d0 = rl * 2 * NP;
+    const size_t frame = (size_t)H * W1 * D;
+    const int16_t* Cf = C + f * frame + d0;
+    AccT* Af = A + f * frame + d0;
+    AccT* dp = dummy + (size_t)threadIdx.x * 2 * NP;
+    const uint32_t p1x2 = (uint32_t)(P1 & 0xffff) * 0x10001u;
+    const uint32_t p2x2 = (uint32_t)(P2 & 0xffff) * 0x10001u;
+    const unsigned tag16 = epoch & 0xffffu;
+    const unsigned long long tag = (unsigned long long)tag16 << 48;
+
+    auto cell_x = [&](int t) { return U - (H - 1) + t; };
+    auto cell_off = [&](int t) -> size_t {
+        const int x = clampi(cell_x(t), 0, W1 - 1);
+        const int y = sy > 0 ? t : H - 1 - t;
+        return ((size_t)y * W1 + x) * D;
+    };
+    auto lcol = [&](int buf, int dir, int c) -> uint32_t* {
+        return lds + (size_t)((buf * 2 + dir) * TL::kCols + c) * TL::kColDw + rl * NP;
+    };
+    auto mcol = [&](int buf, int dir, int c) -> int* { return lmin + (buf * 2 + dir) * TL::kCols + c; };
+
+    // zero both LDS rows (cells outside the image / before the first step)
+    for (int i = threadIdx.x; i < TL::kLDw + TL::kMinInts; i += 64 * kTriWaves) lds[i] = 0u;
+
+    // ---- boundary consumer: wave kTriWaves-1, rows 0..2 (item j = r) ----
+    const bool consumer = w == kTriWaves - 1 && r < 3 && k > 0;
+    const int bcol = kTriSW + (r == 2 ? 1 : 0);  // LDS column the item lands in
+    const int bdir = r == 0 ? 0 : 1;
+    auto bvalid = [&](int t) {
+        const int xx = U0 + bcol - (H - 1) + t;
+        return t >= 0 && xx >= 0 && xx < W1;
+    };
+    const size_t bstep = (size_t)3 * 16 * NG;
+    const unsigned long long* bsrc =
+        bnd + (k > 0 ? tri_slot<NP>(f, k - 1, 0, nframes, H) : 0) + ((size_t)min(r, 2) * 16 + rl) * NG;
+    unsigned long long bg[2][NG];
+    auto bload = [&](int t, unsigned long long (&g)[NG]) {
+        const unsigned long long* q = bsrc + (size_t)clampi(t, 0, H - 1) * bstep;
+#pragma unroll
+        for (int i = 0; i < NG; i++)
+            g[i] = consumer ? __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : tag;
+    };
+    // make item t available in g (spin until the producer's tag shows), then
+    // write it into LDS row `buf`
+    auto bconsume = [&](int t, int buf, unsigned long long (&g)[NG]) {
+        const bool need = consumer && bvalid(t);
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < NG; i++) ok &= !need || (unsigned)(g[i] >> 48) == tag16;
+        unsigned spins = 0;
+        while (!__all(ok)) {  // wave-uniform loop
+            // give up after kTriSpinLimit polls, or at once when any block gave up
+            if (++spins > kTriSpinLimit) {
+                if (lane == 0) atomicOr(status, 1);
+                break;
+            }
+            if ((spins & 63) == 0 &&
+                __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+                break;
+            __builtin_amdgcn_s_sleep(2);
+            if (need && !ok) {
+                const unsigned long long* q = bsrc + (size_t)t * bstep;
+                ok = true;
+#pragma unroll
+                for (int i = 0; i < NG; i++) {
+                    g[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok &= (unsigned)(g[i] >> 48) == tag16;
+                }
+            }
+        }
+        if (w == kTriWaves - 1 && r < 3) {
+            uint32_t v[NP];
+            int mn;
+            TG::unpack(g, v, mn);
+            uint32_t* dst = lcol(buf, bdir, bcol);
+#pragma unroll
+            for (int i = 0; i < NP; i++) dst[i] = need ? v[i] : 0u;
+            if (rl == 0) *mcol(buf, bdir, bcol) = need ? mn : 0;
+        }
+    };
+
+    // ---- producer: wave 0, rows 0..1 publish items for the strip on the left
+    const bool producer = w == 0 && r < 2 && k + 1 < nstrips;
+    unsigned long long* pdst = bnd + tri_slot<NP>(f, k, 0, nframes, H) + (size_t)rl * NG;
+
+    __syncthreads();  // LDS zeroed
+    // boundary of step tb-1 (the right strip's cells the first step reads)
+    bload(tb - 1, bg[1]);
+    bconsume(tb - 1, 1, bg[1]);
+    bload(tb, bg[0]);
+    if (tb + 1 < te) bload(tb + 1, bg[1]);
+
+    uint32_t la[NP];
+#pragma unroll
+    for (int p = 0; p < NP; p++) la[p] = 0u;
+    int ma = 0;
+
+    Vec<NP> cb[PF];
+    uint32_t ab[PF][NP];
+#pragma unroll
+    for (int j = 0; j < PF; j++) {
+        const int t = min(tb + j, te - 1);
+        cb[j].load(Cf + cell_off(t));
+        if (!FIRST) AV::load(Af + cell_off(t), ab[j]);
+    }
+    __syncthreads();
+
+    auto body = [&](int i, int j) {
+        const int t = tb + i;
+        const int cur = i & 1, prv = cur ^ 1;
+        const int x = cell_x(t);
+        const bool valid = x >= 0 && x < W1;
+        uint32_t c[NP];
+#pragma unroll
+        for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
+        uint32_t pb[NP], pc[NP];
+        {
+            const uint32_t* sb = lcol(prv, 0, col + 1);
+            const uint32_t* sc = lcol(prv, 1, col + 2);
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                pb[p] = sb[p];
+                pc[p] = sc[p];
+            }
+        }
+        const int mb = *mcol(prv, 0, col + 1), mc = *mcol(prv, 1, col + 2);
+        uint32_t na[NP], nb[NP], nc[NP];
+        sgm_step_row<NP>(la, (uint32_t)((ma + P2) & 0xffff) * 0x10001u, p1x2, c, na);
+        sgm_step_row<NP>(pb, (uint32_t)((mb + P2) & 0xffff) * 0x10001u, p1x2, c, nb);
+        sgm_step_row<NP>(pc, (uint32_t)((mc + P2) & 0xffff) * 0x10001u, p1x2, c, nc);
+        const int mna = row_min_i32(lane_min_row<NP>(na));
+        const int mnb = row_min_i32(lane_min_row<NP>(nb));
+        const int mnc = row_min_i32(lane_min_row<NP>(nc));
+        uint32_t o[NP];
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            uint32_t dv = path_delta(na[p], c[p], p2x2) + path_delta(nb[p], c[p], p2x2);
+            dv = AV::add(dv, path_delta(nc[p], c[p], p2x2));
+            o[p] = FIRST ? dv : AV::add(ab[j][p], dv);
+            la[p] = valid ? na[p] : 0u;
+            nb[p] = valid ? nb[p] : 0u;
+            nc[p] = valid ? nc[p] : 0u;
+        }
+        ma = valid ? mna : 0;
+        AV::store(valid ? Af + cell_off(t) : dp, o);
+        {
+            uint32_t* db = lcol(cur, 0, col);
+            uint32_t* dc = lcol(cur, 1, col);
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                db[p] = nb[p];
+                dc[p] = nc[p];
+            }
+            if (rl == 0) {
+                *mcol(cur, 0, col) = valid ? mnb : 0;
+                *mcol(cur, 1, col) = valid ? mnc : 0;
+            }
+        }
+        if (producer && valid) {
+            unsigned long long* q = pdst + (size_t)t * bstep;
+            unsigned long long g[NG];
+            if (r == 0) {
+                TG::pack(nb, mnb, tag, g);
+#pragma unroll
+                for (int i = 0; i < NG; i++)
+                    __hip_atomic_store(q + i, g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            TG::pack(nc, mnc, tag, g);
+            unsigned long long* qc = q + (size_t)(1 + r) * 16 * NG;
+#pragma unroll
+            for (int i = 0; i < NG; i++)
+                __hip_atomic_store(qc + i, g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // right strip's step-t items for the next step, then prefetch step t+2
+        if (cur == 0) {
+            bconsume(t, cur, bg[0]);
+            bload(t + 2, bg[0]);
+        } else {
+            bconsume(t, cur, bg[1]);
+            bload(t + 2, bg[1]);
+        }
+        const int tn = min(t + PF, te - 1);
+        cb[j].load(Cf + cell_off(tn));
+        if (!FIRST) AV::load(Af + cell_off(tn), ab[j]);
+        __syncthreads();
+    };
+    const int len = te - tb;
+    int i = 0;
+    for (; i + PF <= len; i += PF) {
+#pragma unroll
+        for (int j = 0; j < PF; j++) body(i + j, j);
+    }
+#pragma unroll
+    for (int j = 0; j < PF; j++)
+        if (i + j < len) body(i + j, j);
 }
 
 // ---------------------------------------------------------------------------
@@ -1393,6 +1697,41 @@ __global__ void fill_s16_kernel(int16_t* __restrict__ out, size_t os, size_t ofs
 }
 
 template <int NP, typename AccT>
+int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, bool first,
+               int sy)
+{
+    using TL = TriLayout<NP>;
+    const int nstrips = (e.W1 + H - 1 + kTriSW - 1) / kTriSW;
+    const size_t bytes = (size_t)n * nstrips * H * 3 * 16 * TriGran<NP>::NG * 8;
+    int rc;
+    if (ctx->tri_bnd.bytes < bytes) {
+        if ((rc = ensure(ctx, ctx->tri_bnd, bytes, "sgbm strip boundary granules"))) return rc;
+        // fresh granules carry epoch 0, which no launch uses
+        if ((rc = check_hip(ctx, hipMemsetAsync(ctx->tri_bnd.ptr, 0, ctx->tri_bnd.bytes, ctx->stream),
+                            "sgbm boundary reset")))
+            return rc;
+    }
+    if (!ctx->status.ptr) {
+        if ((rc = ensure(ctx, ctx->status, 16, "device status word"))) return rc;
+        if ((rc = check_hip(ctx, hipMemsetAsync(ctx->status.ptr, 0, 16, ctx->stream), "status reset")))
+            return rc;
+    }
+    if ((++ctx->tri_epoch & 0xffffu) == 0) ++ctx->tri_epoch;  // tag 0 = never written
+    const unsigned epoch = ctx->tri_epoch;
+    dim3 grid(nstrips * n);
+    StageTimer tm(ctx, kStagePath);
+    if (first)
+        hipLaunchKernelGGL((sgbm_tri_kernel<NP, true, AccT>), grid, dim3(64 * kTriWaves), TL::kBytes,
+                           ctx->stream, Cv, Av, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, sy, e.P1, e.P2,
+                           (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips, (int*)ctx->status.ptr);
+    else
+        hipLaunchKernelGGL((sgbm_tri_kernel<NP, false, AccT>), grid, dim3(64 * kTriWaves), TL::kBytes,
+                           ctx->stream, Cv, Av, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, sy, e.P1, e.P2,
+                           (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips, (int*)ctx->status.ptr);
+    return check_hip(ctx, hipGetLastError(), "sgbm sheared-strip path kernel");
+}
+
+template <int NP, typename AccT>
 int launch_paths16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, AccT* Av,
                    int16_t* raw)
 {
@@ -1400,22 +1739,33 @@ int launch_paths16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t
     static const int dirs_sgbm[4][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}};
     static const int dirs_hh[7][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}, {1, -1}, {0, -1}, {-1, -1}};
     int rc;
-    if ((rc = ensure(ctx, ctx->dummy, 256 * 16 * 2, "sgbm dummy slots"))) return rc;
+    if ((rc = ensure(ctx, ctx->dummy, 512 * 16 * 2 * NP, "sgbm dummy slots"))) return rc;
     if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
     AccT* dummy = (AccT*)ctx->dummy.ptr;
     const int ndir = e.fullDP ? 7 : 4;
-    for (int k = 0; k < ndir; k++) {
-        int dx = e.fullDP ? dirs_hh[k][0] : dirs_sgbm[k][0];
-        int dy = e.fullDP ? dirs_hh[k][1] : dirs_sgbm[k][1];
-        int nl = num_lines(dx, dy, e.W1, H);
-        dim3 grid((nl + 15) / 16, n);
+    if (ctx->tri) {
+        // directions (1,1) (0,1) (-1,1) in one sweep, (1,-1) (0,-1) (-1,-1) in a
+        // second, then L->R; R->L is fused into the final kernel
+        if ((rc = launch_tri<NP, AccT>(ctx, n, H, e, Cv, Av, true, +1))) return rc;
+        if (e.fullDP && (rc = launch_tri<NP, AccT>(ctx, n, H, e, Cv, Av, false, -1))) return rc;
+        dim3 grid((num_lines(1, 0, e.W1, H) + 15) / 16, n);
         StageTimer tm(ctx, kStagePath);
-        if (k == 0)
-            hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT>), grid, dim3(256), 0, s, Cv, Av,
-                               dummy, H, e.W1, e.D, dx, dy, e.P1, e.P2);
-        else
-            hipLaunchKernelGGL((sgbm_path16_kernel<NP, false, AccT>), grid, dim3(256), 0, s, Cv,
-                               Av, dummy, H, e.W1, e.D, dx, dy, e.P1, e.P2);
+        hipLaunchKernelGGL((sgbm_path16_kernel<NP, false, AccT>), grid, dim3(256), 0, s, Cv, Av,
+                           dummy, H, e.W1, e.D, 1, 0, e.P1, e.P2);
+    } else {
+        for (int k = 0; k < ndir; k++) {
+            int dx = e.fullDP ? dirs_hh[k][0] : dirs_sgbm[k][0];
+            int dy = e.fullDP ? dirs_hh[k][1] : dirs_sgbm[k][1];
+            int nl = num_lines(dx, dy, e.W1, H);
+            dim3 grid((nl + 15) / 16, n);
+            StageTimer tm(ctx, kStagePath);
+            if (k == 0)
+                hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT>), grid, dim3(256), 0, s, Cv,
+                                   Av, dummy, H, e.W1, e.D, dx, dy, e.P1, e.P2);
+            else
+                hipLaunchKernelGGL((sgbm_path16_kernel<NP, false, AccT>), grid, dim3(256), 0, s,
+                                   Cv, Av, dummy, H, e.W1, e.D, dx, dy, e.P1, e.P2);
+        }
     }
     StageTimer tm(ctx, kStageFinal);
     hipLaunchKernelGGL((sgbm_final16_kernel<NP, AccT>), dim3((H + 3) / 4, n), dim3(64), 0, s, Cv,
