@@ -346,6 +346,9 @@ void mvsv_destroy(mvsv_ctx* ctx)
     mvsv_trim(ctx);
     mvsv_profile_reset(ctx);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
     delete ctx;
 }

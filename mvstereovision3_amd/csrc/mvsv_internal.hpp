@@ -62,6 +62,8 @@ struct mvsv_ctx {
     // SGBM
     mvsv::DevBuf pre, cost, agg, raw, uf_parent, uf_size, uf_tile, dummy, keys, tri_bnd, status;
     unsigned tri_epoch = 0;  // tag of the strip-boundary granules of the last launch
+    hipStream_t aux = nullptr;  // second stream for concurrent direction passes
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int path16 = 1;  // 16-lanes-per-scanline path kernels where D allows
     int cost2 = 1;   // register-ring cost kernel where blockSize <= 15
     int tri = 1;     // sheared-strip kernels: three directions per sweep

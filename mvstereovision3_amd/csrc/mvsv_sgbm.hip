@@ -20,6 +20,9 @@
 // Data layout in HBM: C and S are [frame][y][x][d] int16 with d contiguous,
 // so one cost column (D = 128 -> 256 B) is one coalesced wave access.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "mvsv_device.hpp"
 #include "mvsv_internal.hpp"
@@ -915,8 +918,8 @@ __device__ __forceinline__ void sgm_step_row(const uint32_t (&lp)[NP], uint32_t 
         uint32_t nl = p == NP - 1 ? next_lo : lp[p + 1];
         uint32_t lm = __builtin_amdgcn_alignbit(lp[p], ph, 16);
         uint32_t lq = __builtin_amdgcn_alignbit(nl, lp[p], 16);
-        uint32_t m = pk_min(lp[p], pk_add_sat(lm, p1x2));
-        m = pk_min(m, pk_add_sat(lq, p1x2));
+        // min(L[d-1] + P1, L[d+1] + P1) == min(L[d-1], L[d+1]) + P1 (saturating add is monotone)
+        uint32_t m = pk_min(lp[p], pk_add_sat(pk_min(lm, lq), p1x2));
         m = pk_min(m, delta2);
         ln[p] = pk_add_sat(pk_sub_sat(m, delta2), c[p]);
     }
@@ -929,6 +932,23 @@ __device__ __forceinline__ int lane_min_row(const uint32_t (&ln)[NP])
 #pragma unroll
     for (int p = 1; p < NP; p++) m = pk_min(m, ln[p]);
     return min(lo16(m), hi16(m));
+}
+
+__device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t b, uint32_t c)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, b) +
+                                            __builtin_bit_cast(u16x2, c));
+}
+
+// Two independent u16 minima over each 16-lane row (packed in one dword).
+__device__ __forceinline__ uint32_t row_min_u16x2(uint32_t v)
+{
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, false));
+    return v;
 }
 
 constexpr int kPath16PF = 12;
@@ -1017,16 +1037,19 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
 // strip one step per row -- every step is SW contiguous x-columns of C and of
 // the accumulator -- and needs only the two U-columns right of it from the
 // previous step: the strip to its right (lower block index) publishes them as
-// 8-byte {epoch, value} granules with write-through stores, this strip polls
-// them (bounded spin).  C and the accumulator are read once for three
-// directions instead of three times.  Cells outside the image carry L = 0,
-// min 0: exactly the zero start state of every path at the image border.
-// Lanes: 16 per U-column (2*NP disparities each), 4 columns per wave, SWW
-// waves per block; neighbours in U go through a double-buffered LDS row.
+// tagged 8-byte granules with write-through stores, this strip polls them
+// (bounded spin).  C is read once for three directions instead of three
+// times.  Cells outside the image carry L = 0, min 0: exactly the zero start
+// state of every path at the image border.
+// Lanes: 16 per U-column (2*NP disparities each), 4 columns per compute wave;
+// one extra wave per block does all strip-to-strip traffic, so the compute
+// waves' memory counters only ever wait for their own C loads.
 // ---------------------------------------------------------------------------
-constexpr int kTriWaves = 8;
+constexpr int kTriWaves = 8;            // compute waves
 constexpr int kTriSW = 4 * kTriWaves;  // U-columns per strip
-constexpr int kTriPF = 2;               // steps of C / accumulator prefetch
+constexpr int kTriPF = 2;               // steps of C prefetch (compute waves)
+constexpr int kTriBF = 2;               // steps of boundary prefetch (comm wave)
+constexpr int kTriUnroll = 2;           // lcm(kTriPF, kTriBF, 2)
 constexpr unsigned kTriSpinLimit = 1u << 16;
 
 template <int NP>
@@ -1039,11 +1062,12 @@ struct TriLayout {
     static constexpr size_t kBytes = (size_t)(kLDw + kMinInts) * 4;
 };
 
-// Boundary granules of one strip and step: [3 items][16 lanes][NG] u64.
-// Item 0 = L of dir (0, sy) at the strip's first column, 1 = dir (-1, sy) at
-// the first column, 2 = dir (-1, sy) at the second column.  A lane's item is
-// its 2*NP int16 costs + the column min, three int16 per granule under a
-// 16-bit launch tag (bits 48-63): the tag is the data-ready flag.
+// Boundary granules of one strip and step: [3 items][16 lanes][NG] u64 (+ one
+// spare item row the comm wave's idle lanes store into).  Item 0 = L of dir
+// (0, sy) at the strip's first column, 1 = dir (-1, sy) at the first column,
+// 2 = dir (-1, sy) at the second column.  A lane's item is its 2*NP int16
+// costs + the column min, three int16 per granule under a 16-bit launch tag
+// (bits 48-63): the tag is the data-ready flag.
 template <int NP>
 struct TriGran {
     static constexpr int NG = (2 * NP + 1 + 2) / 3;
@@ -1080,187 +1104,227 @@ struct TriGran {
 };
 
 template <int NP>
-__device__ __forceinline__ size_t tri_slot(int f, int k, int t, int nframes, int H)
+__device__ __forceinline__ size_t tri_slot(int chain, int k, int t, int nchains, int H)
 {
-    return ((((size_t)k * nframes + f) * H + t) * 3) * 16 * TriGran<NP>::NG;
+    return ((((size_t)k * nchains + chain) * H + t) * 4) * 16 * TriGran<NP>::NG;
 }
 
-template <int NP, bool FIRST, typename AccT>
-__global__ __launch_bounds__(64 * kTriWaves) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
-    const int16_t* __restrict__ C, AccT* __restrict__ A, AccT* __restrict__ dummy, int H, int W1,
-    int D, int sy, int P1, int P2, unsigned long long* __restrict__ bnd, unsigned epoch,
-    int nframes, int nstrips, int* __restrict__ status)
+template <int NP, typename AccT>
+__global__ __launch_bounds__(64 * (kTriWaves + 1))
+__attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
+    const int16_t* __restrict__ C, AccT* __restrict__ A, size_t plane, AccT* __restrict__ dummy,
+    int H, int W1, int D, int npass, int P1, int P2, unsigned long long* __restrict__ bnd,
+    unsigned epoch, int nframes, int nstrips, int* __restrict__ status,
+    unsigned long long* __restrict__ stats)
 {
     using AV = AccVec<NP, AccT>;
     using TL = TriLayout<NP>;
     using TG = TriGran<NP>;
     constexpr int NG = TG::NG;
     constexpr int PF = kTriPF;
+    constexpr int BF = kTriBF;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* lds = (uint32_t*)smem;
     int* lmin = (int*)(lds + TL::kLDw);
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool comm = w == kTriWaves;
     const int r = lane >> 4, rl = lane & 15;
-    // strips counted from the right, frames interleaved: every block's
-    // producer (same frame, strip k-1) has a lower block index
-    const int k = blockIdx.x / nframes;
-    const int f = blockIdx.x - k * nframes;
+    // strips counted from the right; passes and frames interleaved, so every
+    // block's producer (same pass and frame, strip k-1) has a lower index.
+    // Pass 0 sweeps down (sy = +1), pass 1 up (sy = -1), each into its own
+    // accumulator plane.
+    const int nchains = npass * nframes;
+    const int k = blockIdx.x / nchains;
+    const int chain = blockIdx.x - k * nchains;
+    const int pass = chain / nframes;
+    const int f = chain - pass * nframes;
+    const int sy = pass == 0 ? 1 : -1;
+    A += pass * plane;
     const int Utot = W1 + H - 1;
     const int U0 = Utot - kTriSW * (k + 1);
-    const int col = 4 * w + r;
+    const int col = 4 * w + r;  // compute waves
     const int U = U0 + col;
     // active steps: some column of the strip has 0 <= x = U - (H-1) + t < W1
     const int tb = max(0, (H - 1) - (U0 + kTriSW - 1));
     const int te = min(H, W1 + (H - 1) - U0);
     if (tb >= te) return;
+    unsigned long long st_t0 = stats ? __builtin_amdgcn_s_memtime() : 0ull, st_spin = 0, st_n = 0;
     const int d0 = rl * 2 * NP;
     const size_t frame = (size_t)H * W1 * D;
     const int16_t* Cf = C + f * frame + d0;
     AccT* Af = A + f * frame + d0;
     AccT* dp = dummy + (size_t)threadIdx.x * 2 * NP;
     const uint32_t p1x2 = (uint32_t)(P1 & 0xffff) * 0x10001u;
-    const uint32_t p2x2 = (uint32_t)(P2 & 0xffff) * 0x10001u;
+    // -3 * (C - P2) = C * 0xFFFD + 3 * P2 (mod 2^16)
+    const uint32_t p2x3 = (uint32_t)((3 * P2) & 0xffff) * 0x10001u;
     const unsigned tag16 = epoch & 0xffffu;
     const unsigned long long tag = (unsigned long long)tag16 << 48;
 
-    auto cell_x = [&](int t) { return U - (H - 1) + t; };
-    auto cell_off = [&](int t) -> size_t {
-        const int x = clampi(cell_x(t), 0, W1 - 1);
-        const int y = sy > 0 ? t : H - 1 - t;
-        return ((size_t)y * W1 + x) * D;
-    };
     auto lcol = [&](int buf, int dir, int c) -> uint32_t* {
         return lds + (size_t)((buf * 2 + dir) * TL::kCols + c) * TL::kColDw + rl * NP;
     };
     auto mcol = [&](int buf, int dir, int c) -> int* { return lmin + (buf * 2 + dir) * TL::kCols + c; };
 
     // zero both LDS rows (cells outside the image / before the first step)
-    for (int i = threadIdx.x; i < TL::kLDw + TL::kMinInts; i += 64 * kTriWaves) lds[i] = 0u;
+    for (int i = threadIdx.x; i < TL::kLDw + TL::kMinInts; i += 64 * (kTriWaves + 1)) lds[i] = 0u;
 
-    // ---- boundary consumer: wave kTriWaves-1, rows 0..2 (item j = r) ----
-    const bool consumer = w == kTriWaves - 1 && r < 3 && k > 0;
-    const int bcol = kTriSW + (r == 2 ? 1 : 0);  // LDS column the item lands in
-    const int bdir = r == 0 ? 0 : 1;
+    // ---- comm wave: lanes (item j = min(r, 2), rl); row 3 duplicates item 2's
+    // loads and stores into the spare item row, so every comm-wave memory
+    // instruction is unpredicated and its wait counts are exact.
+    const int jj = min(r, 2);
+    const bool jlive = r < 3;
+    const int bcol = kTriSW + (jj == 2 ? 1 : 0);  // LDS column the consumed item lands in
+    const int bdir = jj == 0 ? 0 : 1;
+    const int pcol = jj == 2 ? 1 : 0;              // own column published as item jj
+    const size_t bstep = (size_t)4 * 16 * NG;
+    const unsigned long long* bsrc =
+        bnd + tri_slot<NP>(chain, k > 0 ? k - 1 : k, 0, nchains, H) + ((size_t)jj * 16 + rl) * NG;
+    unsigned long long* pdst = bnd + tri_slot<NP>(chain, k, 0, nchains, H) + ((size_t)r * 16 + rl) * NG;
     auto bvalid = [&](int t) {
         const int xx = U0 + bcol - (H - 1) + t;
-        return t >= 0 && xx >= 0 && xx < W1;
+        return k > 0 && t >= 0 && xx >= 0 && xx < W1;
     };
-    const size_t bstep = (size_t)3 * 16 * NG;
-    const unsigned long long* bsrc =
-        bnd + (k > 0 ? tri_slot<NP>(f, k - 1, 0, nframes, H) : 0) + ((size_t)min(r, 2) * 16 + rl) * NG;
-    unsigned long long bg[2][NG];
     auto bload = [&](int t, unsigned long long (&g)[NG]) {
         const unsigned long long* q = bsrc + (size_t)clampi(t, 0, H - 1) * bstep;
 #pragma unroll
-        for (int i = 0; i < NG; i++)
-            g[i] = consumer ? __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                            : tag;
+        for (int i = 0; i < NG; i++) g[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    // make item t available in g (spin until the producer's tag shows), then
-    // write it into LDS row `buf`
+    // item t into LDS row buf, spinning until the producer's tag shows
     auto bconsume = [&](int t, int buf, unsigned long long (&g)[NG]) {
-        const bool need = consumer && bvalid(t);
+        const bool need = jlive && bvalid(t);
         bool ok = true;
 #pragma unroll
         for (int i = 0; i < NG; i++) ok &= !need || (unsigned)(g[i] >> 48) == tag16;
-        unsigned spins = 0;
-        while (!__all(ok)) {  // wave-uniform loop
-            // give up after kTriSpinLimit polls, or at once when any block gave up
-            if (++spins > kTriSpinLimit) {
-                if (lane == 0) atomicOr(status, 1);
-                break;
-            }
-            if ((spins & 63) == 0 &&
-                __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
-                break;
-            __builtin_amdgcn_s_sleep(2);
-            if (need && !ok) {
-                const unsigned long long* q = bsrc + (size_t)t * bstep;
+        if (!__all(ok)) {
+            const unsigned long long sp0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+            unsigned spins = 0;
+            while (!__all(ok)) {
+                // give up after kTriSpinLimit polls, or at once when any block gave up
+                if (++spins > kTriSpinLimit) {
+                    if (lane == 0) atomicOr(status, 1);
+                    break;
+                }
+                if ((spins & 63) == 0 &&
+                    __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+                    break;
+                __builtin_amdgcn_s_sleep(1);
+                const unsigned long long* q = bsrc + (size_t)clampi(t, 0, H - 1) * bstep;
                 ok = true;
 #pragma unroll
                 for (int i = 0; i < NG; i++) {
                     g[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok &= (unsigned)(g[i] >> 48) == tag16;
+                    ok &= !need || (unsigned)(g[i] >> 48) == tag16;
                 }
             }
+            if (stats) {
+                st_spin += __builtin_amdgcn_s_memtime() - sp0;
+                st_n += spins;
+            }
         }
-        if (w == kTriWaves - 1 && r < 3) {
-            uint32_t v[NP];
-            int mn;
-            TG::unpack(g, v, mn);
+        uint32_t v[NP];
+        int mn;
+        TG::unpack(g, v, mn);
+        if (jlive) {
             uint32_t* dst = lcol(buf, bdir, bcol);
 #pragma unroll
             for (int i = 0; i < NP; i++) dst[i] = need ? v[i] : 0u;
             if (rl == 0) *mcol(buf, bdir, bcol) = need ? mn : 0;
         }
     };
+    // publish step t of this strip's columns 0 and 1 (LDS row buf) for the left
+    // strip; unconditional stores (idle lanes and unused steps hit unread slots)
+    auto publish = [&](int t, int buf) {
+        uint32_t v[NP];
+        const uint32_t* src = lcol(buf, bdir, pcol);
+#pragma unroll
+        for (int i = 0; i < NP; i++) v[i] = src[i];
+        const int mn = *mcol(buf, bdir, pcol);
+        unsigned long long g[NG];
+        TG::pack(v, mn, tag, g);
+        unsigned long long* q = pdst + (size_t)clampi(t, 0, H - 1) * bstep;
+#pragma unroll
+        for (int i = 0; i < NG; i++) __hip_atomic_store(q + i, g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
 
-    // ---- producer: wave 0, rows 0..1 publish items for the strip on the left
-    const bool producer = w == 0 && r < 2 && k + 1 < nstrips;
-    unsigned long long* pdst = bnd + tri_slot<NP>(f, k, 0, nframes, H) + (size_t)rl * NG;
-
-    __syncthreads();  // LDS zeroed
-    // boundary of step tb-1 (the right strip's cells the first step reads)
-    bload(tb - 1, bg[1]);
-    bconsume(tb - 1, 1, bg[1]);
-    bload(tb, bg[0]);
-    if (tb + 1 < te) bload(tb + 1, bg[1]);
-
+    // ---- compute waves ----
+    auto cell_x = [&](int t) { return U - (H - 1) + t; };
+    auto cell_off = [&](int t) -> size_t {
+        const int x = clampi(cell_x(t), 0, W1 - 1);
+        const int y = sy > 0 ? t : H - 1 - t;
+        return ((size_t)y * W1 + x) * D;
+    };
     uint32_t la[NP];
 #pragma unroll
     for (int p = 0; p < NP; p++) la[p] = 0u;
     int ma = 0;
-
     Vec<NP> cb[PF];
-    uint32_t ab[PF][NP];
+    unsigned long long bg[BF][NG];
+
+    __syncthreads();  // LDS zeroed
+    if (comm) {
+        bload(tb - 1, bg[0]);
+        bconsume(tb - 1, 1, bg[0]);  // the right strip's cells the first step reads
 #pragma unroll
-    for (int j = 0; j < PF; j++) {
-        const int t = min(tb + j, te - 1);
-        cb[j].load(Cf + cell_off(t));
-        if (!FIRST) AV::load(Af + cell_off(t), ab[j]);
+        for (int j = 0; j < BF; j++) bload(tb + j, bg[j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < PF; j++) cb[j].load(Cf + cell_off(min(tb + j, te - 1)));
     }
     __syncthreads();
 
-    auto body = [&](int i, int j) {
+    auto step = [&](int i, int j) {
         const int t = tb + i;
         const int cur = i & 1, prv = cur ^ 1;
-        const int x = cell_x(t);
-        const bool valid = x >= 0 && x < W1;
-        uint32_t c[NP];
+        if (comm) {
+            if (i > 0) publish(t - 1, prv);
+            bconsume(t, cur, bg[j % BF]);
+            bload(t + BF, bg[j % BF]);
+        } else {
+            const int x = cell_x(t);
+            const bool valid = x >= 0 && x < W1;
+            uint32_t c[NP];
 #pragma unroll
-        for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
-        uint32_t pb[NP], pc[NP];
-        {
-            const uint32_t* sb = lcol(prv, 0, col + 1);
-            const uint32_t* sc = lcol(prv, 1, col + 2);
+            for (int p = 0; p < NP; p++) c[p] = cb[j % PF].v[p];
+            cb[j % PF].load(Cf + cell_off(min(t + PF, te - 1)));
+            uint32_t pb[NP], pc[NP];
+            {
+                const uint32_t* sb = lcol(prv, 0, col + 1);
+                const uint32_t* sc = lcol(prv, 1, col + 2);
+#pragma unroll
+                for (int p = 0; p < NP; p++) {
+                    pb[p] = sb[p];
+                    pc[p] = sc[p];
+                }
+            }
+            const int mb = *mcol(prv, 0, col + 1), mc = *mcol(prv, 1, col + 2);
+            uint32_t na[NP], nb[NP], nc[NP];
+            sgm_step_row<NP>(la, (uint32_t)((ma + P2) & 0xffff) * 0x10001u, p1x2, c, na);
+            sgm_step_row<NP>(pb, (uint32_t)((mb + P2) & 0xffff) * 0x10001u, p1x2, c, nb);
+            sgm_step_row<NP>(pc, (uint32_t)((mc + P2) & 0xffff) * 0x10001u, p1x2, c, nc);
+            const int mna = row_min_i32(lane_min_row<NP>(na));
+            // the b and c minima share one packed row reduction (values <= 32767)
+            const uint32_t mbc = row_min_u16x2((uint32_t)lane_min_row<NP>(nb) |
+                                               ((uint32_t)lane_min_row<NP>(nc) << 16));
+            uint32_t o[NP];
 #pragma unroll
             for (int p = 0; p < NP; p++) {
-                pb[p] = sb[p];
-                pc[p] = sc[p];
+                // sum of the three deltas L - (C - P2), exact in u16 wrap arithmetic
+                const uint32_t c3n = pk_mad_u16(c[p], 0xfffdfffdu, p2x3);  // 3 * P2 - 3 * C
+                o[p] = pk_add_u16(pk_add_u16(na[p], nb[p]), pk_add_u16(nc[p], c3n));
             }
-        }
-        const int mb = *mcol(prv, 0, col + 1), mc = *mcol(prv, 1, col + 2);
-        uint32_t na[NP], nb[NP], nc[NP];
-        sgm_step_row<NP>(la, (uint32_t)((ma + P2) & 0xffff) * 0x10001u, p1x2, c, na);
-        sgm_step_row<NP>(pb, (uint32_t)((mb + P2) & 0xffff) * 0x10001u, p1x2, c, nb);
-        sgm_step_row<NP>(pc, (uint32_t)((mc + P2) & 0xffff) * 0x10001u, p1x2, c, nc);
-        const int mna = row_min_i32(lane_min_row<NP>(na));
-        const int mnb = row_min_i32(lane_min_row<NP>(nb));
-        const int mnc = row_min_i32(lane_min_row<NP>(nc));
-        uint32_t o[NP];
+            AV::store(valid ? Af + cell_off(t) : dp, o);
+            if (__builtin_expect(!__all(valid), 0)) {
 #pragma unroll
-        for (int p = 0; p < NP; p++) {
-            uint32_t dv = path_delta(na[p], c[p], p2x2) + path_delta(nb[p], c[p], p2x2);
-            dv = AV::add(dv, path_delta(nc[p], c[p], p2x2));
-            o[p] = FIRST ? dv : AV::add(ab[j][p], dv);
-            la[p] = valid ? na[p] : 0u;
-            nb[p] = valid ? nb[p] : 0u;
-            nc[p] = valid ? nc[p] : 0u;
-        }
-        ma = valid ? mna : 0;
-        AV::store(valid ? Af + cell_off(t) : dp, o);
-        {
+                for (int p = 0; p < NP; p++) {
+                    na[p] = valid ? na[p] : 0u;
+                    nb[p] = valid ? nb[p] : 0u;
+                    nc[p] = valid ? nc[p] : 0u;
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < NP; p++) la[p] = na[p];
+            ma = valid ? mna : 0;
             uint32_t* db = lcol(cur, 0, col);
             uint32_t* dc = lcol(cur, 1, col);
 #pragma unroll
@@ -1269,47 +1333,35 @@ __global__ __launch_bounds__(64 * kTriWaves) __attribute__((amdgpu_waves_per_eu(
                 dc[p] = nc[p];
             }
             if (rl == 0) {
-                *mcol(cur, 0, col) = valid ? mnb : 0;
-                *mcol(cur, 1, col) = valid ? mnc : 0;
+                *mcol(cur, 0, col) = valid ? (int)(mbc & 0xffffu) : 0;
+                *mcol(cur, 1, col) = valid ? (int)(mbc >> 16) : 0;
             }
         }
-        if (producer && valid) {
-            unsigned long long* q = pdst + (size_t)t * bstep;
-            unsigned long long g[NG];
-            if (r == 0) {
-                TG::pack(nb, mnb, tag, g);
-#pragma unroll
-                for (int i = 0; i < NG; i++)
-                    __hip_atomic_store(q + i, g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            TG::pack(nc, mnc, tag, g);
-            unsigned long long* qc = q + (size_t)(1 + r) * 16 * NG;
-#pragma unroll
-            for (int i = 0; i < NG; i++)
-                __hip_atomic_store(qc + i, g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // right strip's step-t items for the next step, then prefetch step t+2
-        if (cur == 0) {
-            bconsume(t, cur, bg[0]);
-            bload(t + 2, bg[0]);
-        } else {
-            bconsume(t, cur, bg[1]);
-            bload(t + 2, bg[1]);
-        }
-        const int tn = min(t + PF, te - 1);
-        cb[j].load(Cf + cell_off(tn));
-        if (!FIRST) AV::load(Af + cell_off(tn), ab[j]);
         __syncthreads();
     };
     const int len = te - tb;
     int i = 0;
-    for (; i + PF <= len; i += PF) {
+    for (; i + kTriUnroll <= len; i += kTriUnroll) {
 #pragma unroll
-        for (int j = 0; j < PF; j++) body(i + j, j);
+        for (int j = 0; j < kTriUnroll; j++) step(i + j, j);
     }
 #pragma unroll
-    for (int j = 0; j < PF; j++)
-        if (i + j < len) body(i + j, j);
+    for (int j = 0; j < kTriUnroll; j++)
+        if (i + j < len) step(i + j, j);
+    if (comm) {
+        publish(te - 1, (len - 1) & 1);
+        if (stats && lane == 0) {
+            unsigned long long* q = stats + (size_t)blockIdx.x * 8;
+            q[0] = st_t0;
+            q[1] = __builtin_amdgcn_s_memtime();
+            q[2] = st_spin;
+            q[3] = st_n;
+            q[4] = (unsigned long long)len;
+            q[5] = (unsigned long long)k;
+            q[6] = (unsigned long long)pass;
+            q[7] = (unsigned long long)tb;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1320,10 +1372,13 @@ __global__ __launch_bounds__(64 * kTriWaves) __attribute__((amdgpu_waves_per_eu(
 // ---------------------------------------------------------------------------
 constexpr int kFinal16PF = 4;
 
-template <int NP, typename AccT>
+// NACC accumulator planes (A + i * plane) hold the summed deltas of disjoint
+// direction groups written by concurrent passes; their sum is the S input.
+template <int NP, int NACC, typename AccT>
 __global__ __launch_bounds__(64) void sgbm_final16_kernel(const int16_t* __restrict__ C,
-                                                         const AccT* __restrict__ A, int H, int W,
-                                                         SgbmEff e, int16_t* __restrict__ raw,
+                                                         const AccT* __restrict__ A, size_t plane,
+                                                         int H, int W, SgbmEff e,
+                                                         int16_t* __restrict__ raw,
                                                          uint32_t* __restrict__ keys)
 {
     using AV = AccVec<NP, AccT>;
@@ -1365,11 +1420,21 @@ __global__ __launch_bounds__(64) void sgbm_final16_kernel(const int16_t* __restr
 
     Vec<NP> cb[PF];
     uint32_t sb[PF][NP];
+    auto acc_load = [&](const AccT* q, uint32_t (&v)[NP]) {
+        AV::load(q, v);
+#pragma unroll
+        for (int i = 1; i < NACC; i++) {
+            uint32_t u[NP];
+            AV::load(q + i * plane, u);
+#pragma unroll
+            for (int p = 0; p < NP; p++) v[p] = AV::add(v[p], u[p]);
+        }
+    };
 #pragma unroll
     for (int j = 0; j < PF; j++) {
         const ptrdiff_t t = min(j, W1 - 1);
         cb[j].load(cp - t * D);
-        AV::load(sp - t * D, sb[j]);
+        acc_load(sp - t * D, sb[j]);
     }
     // Per step the row's 16 lanes agree on K = (minS << 16 | lane-rule sub),
     // S[best-1], S[best+1] and the uniqueness verdict; lane (s & 15) keeps them,
@@ -1472,7 +1537,7 @@ __global__ __launch_bounds__(64) void sgbm_final16_kernel(const int16_t* __restr
             body(s + j, j % PF);
             const ptrdiff_t t = min(s + j + PF, W1 - 1);
             cb[j % PF].load(cp - t * D);
-            AV::load(sp - t * D, sb[j % PF]);
+            acc_load(sp - t * D, sb[j % PF]);
         }
         flush(s, 16);
     }
@@ -1483,7 +1548,7 @@ __global__ __launch_bounds__(64) void sgbm_final16_kernel(const int16_t* __restr
             body(s + j, j % PF);
             const ptrdiff_t t = min(s + j + PF, W1 - 1);
             cb[j % PF].load(cp - t * D);
-            AV::load(sp - t * D, sb[j % PF]);
+            acc_load(sp - t * D, sb[j % PF]);
         }
     }
     if (rem > 0) flush(s, rem);
@@ -1697,16 +1762,16 @@ __global__ void fill_s16_kernel(int16_t* __restrict__ out, size_t os, size_t ofs
 }
 
 template <int NP, typename AccT>
-int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, bool first,
-               int sy)
+int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
+               int npass)
 {
     using TL = TriLayout<NP>;
     const int nstrips = (e.W1 + H - 1 + kTriSW - 1) / kTriSW;
-    const size_t bytes = (size_t)n * nstrips * H * 3 * 16 * TriGran<NP>::NG * 8;
+    const size_t bytes = (size_t)npass * n * nstrips * H * 4 * 16 * TriGran<NP>::NG * 8;
     int rc;
     if (ctx->tri_bnd.bytes < bytes) {
         if ((rc = ensure(ctx, ctx->tri_bnd, bytes, "sgbm strip boundary granules"))) return rc;
-        // fresh granules carry epoch 0, which no launch uses
+        // fresh granules carry tag 0, which no launch uses
         if ((rc = check_hip(ctx, hipMemsetAsync(ctx->tri_bnd.ptr, 0, ctx->tri_bnd.bytes, ctx->stream),
                             "sgbm boundary reset")))
             return rc;
@@ -1718,17 +1783,87 @@ int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT*
     }
     if ((++ctx->tri_epoch & 0xffffu) == 0) ++ctx->tri_epoch;  // tag 0 = never written
     const unsigned epoch = ctx->tri_epoch;
-    dim3 grid(nstrips * n);
-    StageTimer tm(ctx, kStagePath);
-    if (first)
-        hipLaunchKernelGGL((sgbm_tri_kernel<NP, true, AccT>), grid, dim3(64 * kTriWaves), TL::kBytes,
-                           ctx->stream, Cv, Av, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, sy, e.P1, e.P2,
-                           (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips, (int*)ctx->status.ptr);
+    dim3 grid(nstrips * npass * n);
+    unsigned long long* stats = nullptr;
+    const bool want_stats = std::getenv("MVSV_TRI_STATS") != nullptr;
+    if (want_stats) {
+        (void)hipMalloc(&stats, (size_t)grid.x * 64);
+        (void)hipMemset(stats, 0, (size_t)grid.x * 64);
+    }
+    hipLaunchKernelGGL((sgbm_tri_kernel<NP, AccT>), grid, dim3(64 * (kTriWaves + 1)), TL::kBytes,
+                       ctx->stream, Cv, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, npass, e.P1,
+                       e.P2, (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips,
+                       (int*)ctx->status.ptr, stats);
+    rc = check_hip(ctx, hipGetLastError(), "sgbm sheared-strip path kernel");
+    if (want_stats) {
+        (void)hipStreamSynchronize(ctx->stream);
+        std::vector<unsigned long long> h((size_t)grid.x * 8);
+        (void)hipMemcpy(h.data(), stats, h.size() * 8, hipMemcpyDeviceToHost);
+        (void)hipFree(stats);
+        unsigned long long t0 = ~0ull, t1 = 0, spin = 0, busy = 0, steps = 0, longest = 0, lst = 0;
+        for (size_t b = 0; b < grid.x; b++) {
+            const unsigned long long* q = &h[b * 8];
+            if (!q[1]) continue;
+            t0 = std::min(t0, q[0]);
+            t1 = std::max(t1, q[1]);
+            spin += q[2];
+            busy += q[1] - q[0];
+            steps += q[4];
+            if (q[4] > longest) { longest = q[4]; lst = q[1] - q[0]; }
+        }
+        std::fprintf(stderr, "[tri] span %llu ticks, blocks %u, block-ticks %llu, spin-ticks %llu (%.1f%%), "
+                     "ticks/step %.1f, longest strip %llu steps in %llu ticks\n",
+                     t1 - t0, grid.x, busy, spin, 100.0 * spin / std::max(busy, 1ull),
+                     (double)busy / std::max(steps, 1ull), longest, lst);
+        for (size_t b = 0; b < grid.x; b += grid.x / 24 + 1) {
+            const unsigned long long* q = &h[b * 8];
+            std::fprintf(stderr, "[tri]  blk %zu k %llu pass %llu tb %llu len %llu start %llu dur %llu spin %llu n %llu\n",
+                         b, q[5], q[6], q[7], q[4], q[0] - t0, q[1] - q[0], q[2], q[3]);
+        }
+    }
+    return rc;
+}
+
+// Sheared-strip schedule: the down pass ((1,1) (0,1) (-1,1)), the up pass
+// ((1,-1) (0,-1) (-1,-1), MODE_HH) and the L->R lines each write their own
+// accumulator plane; the L->R lines run on a second stream beside the strip
+// kernel, and the final kernel (R->L + WTA) sums the planes.
+template <int NP, typename AccT>
+int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, AccT* Av,
+                     size_t plane, int16_t* raw)
+{
+    hipStream_t s = ctx->stream;
+    int rc;
+    if (!ctx->aux) {
+        if ((rc = check_hip(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking), "aux stream")) ||
+            (rc = check_hip(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming), "event")) ||
+            (rc = check_hip(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming), "event")))
+            return rc;
+    }
+    const int npass = e.fullDP ? 2 : 1;
+    AccT* dummy = (AccT*)ctx->dummy.ptr;
+    {
+        StageTimer tm(ctx, kStagePath);
+        if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_fork, s), "fork")) ||
+            (rc = check_hip(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0), "fork wait")))
+            return rc;
+        dim3 grid((num_lines(1, 0, e.W1, H) + 15) / 16, n);
+        hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT>), grid, dim3(256), 0, ctx->aux, Cv,
+                           Av + npass * plane, dummy, H, e.W1, e.D, 1, 0, e.P1, e.P2);
+        if ((rc = check_hip(ctx, hipGetLastError(), "sgbm L->R lines"))) return rc;
+        if ((rc = launch_tri<NP, AccT>(ctx, n, H, e, Cv, Av, plane, npass))) return rc;
+        if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_join, ctx->aux), "join")) ||
+            (rc = check_hip(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0), "join wait")))
+            return rc;
+    }
+    StageTimer tm(ctx, kStageFinal);
+    if (npass == 2)
+        hipLaunchKernelGGL((sgbm_final16_kernel<NP, 3, AccT>), dim3((H + 3) / 4, n), dim3(64), 0, s,
+                           Cv, Av, plane, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
     else
-        hipLaunchKernelGGL((sgbm_tri_kernel<NP, false, AccT>), grid, dim3(64 * kTriWaves), TL::kBytes,
-                           ctx->stream, Cv, Av, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, sy, e.P1, e.P2,
-                           (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips, (int*)ctx->status.ptr);
-    return check_hip(ctx, hipGetLastError(), "sgbm sheared-strip path kernel");
+        hipLaunchKernelGGL((sgbm_final16_kernel<NP, 2, AccT>), dim3((H + 3) / 4, n), dim3(64), 0, s,
+                           Cv, Av, plane, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
+    return check_hip(ctx, hipGetLastError(), "sgbm path kernels (sheared strips)");
 }
 
 template <int NP, typename AccT>
@@ -1742,34 +1877,25 @@ int launch_paths16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t
     if ((rc = ensure(ctx, ctx->dummy, 512 * 16 * 2 * NP, "sgbm dummy slots"))) return rc;
     if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
     AccT* dummy = (AccT*)ctx->dummy.ptr;
+    const size_t plane = (size_t)n * H * e.W1 * e.D;
+    if (ctx->tri) return launch_paths_tri<NP, AccT>(ctx, n, H, W, e, Cv, Av, plane, raw);
     const int ndir = e.fullDP ? 7 : 4;
-    if (ctx->tri) {
-        // directions (1,1) (0,1) (-1,1) in one sweep, (1,-1) (0,-1) (-1,-1) in a
-        // second, then L->R; R->L is fused into the final kernel
-        if ((rc = launch_tri<NP, AccT>(ctx, n, H, e, Cv, Av, true, +1))) return rc;
-        if (e.fullDP && (rc = launch_tri<NP, AccT>(ctx, n, H, e, Cv, Av, false, -1))) return rc;
-        dim3 grid((num_lines(1, 0, e.W1, H) + 15) / 16, n);
+    for (int k = 0; k < ndir; k++) {
+        int dx = e.fullDP ? dirs_hh[k][0] : dirs_sgbm[k][0];
+        int dy = e.fullDP ? dirs_hh[k][1] : dirs_sgbm[k][1];
+        int nl = num_lines(dx, dy, e.W1, H);
+        dim3 grid((nl + 15) / 16, n);
         StageTimer tm(ctx, kStagePath);
-        hipLaunchKernelGGL((sgbm_path16_kernel<NP, false, AccT>), grid, dim3(256), 0, s, Cv, Av,
-                           dummy, H, e.W1, e.D, 1, 0, e.P1, e.P2);
-    } else {
-        for (int k = 0; k < ndir; k++) {
-            int dx = e.fullDP ? dirs_hh[k][0] : dirs_sgbm[k][0];
-            int dy = e.fullDP ? dirs_hh[k][1] : dirs_sgbm[k][1];
-            int nl = num_lines(dx, dy, e.W1, H);
-            dim3 grid((nl + 15) / 16, n);
-            StageTimer tm(ctx, kStagePath);
-            if (k == 0)
-                hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT>), grid, dim3(256), 0, s, Cv,
-                                   Av, dummy, H, e.W1, e.D, dx, dy, e.P1, e.P2);
-            else
-                hipLaunchKernelGGL((sgbm_path16_kernel<NP, false, AccT>), grid, dim3(256), 0, s,
-                                   Cv, Av, dummy, H, e.W1, e.D, dx, dy, e.P1, e.P2);
-        }
+        if (k == 0)
+            hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT>), grid, dim3(256), 0, s, Cv, Av,
+                               dummy, H, e.W1, e.D, dx, dy, e.P1, e.P2);
+        else
+            hipLaunchKernelGGL((sgbm_path16_kernel<NP, false, AccT>), grid, dim3(256), 0, s, Cv,
+                               Av, dummy, H, e.W1, e.D, dx, dy, e.P1, e.P2);
     }
     StageTimer tm(ctx, kStageFinal);
-    hipLaunchKernelGGL((sgbm_final16_kernel<NP, AccT>), dim3((H + 3) / 4, n), dim3(64), 0, s, Cv,
-                       Av, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
+    hipLaunchKernelGGL((sgbm_final16_kernel<NP, 1, AccT>), dim3((H + 3) / 4, n), dim3(64), 0, s, Cv,
+                       Av, plane, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels (16-lane)");
 }
 
@@ -1917,7 +2043,10 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     const size_t vol = (size_t)e.W1 * H * e.D;
     if ((rc = ensure(ctx, ctx->pre, (size_t)n * 2 * plane * 8, "sgbm BT interval planes"))) return rc;
     if ((rc = ensure(ctx, ctx->cost, (size_t)n * vol * 2, "sgbm cost volume"))) return rc;
-    if ((rc = ensure(ctx, ctx->agg, (size_t)n * vol * (acc_is_u8(e) ? 1 : 2),
+    // accumulator planes: one per concurrently written direction group
+    const bool wide16 = ctx->path16 && (e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256);
+    const int nplanes = (wide16 && ctx->tri) ? (e.fullDP ? 3 : 2) : 1;
+    if ((rc = ensure(ctx, ctx->agg, (size_t)nplanes * n * vol * (acc_is_u8(e) ? 1 : 2),
                      "sgbm path-delta accumulator")))
         return rc;
     if ((rc = ensure(ctx, ctx->raw, (size_t)n * plane * 2, "sgbm raw disparity"))) return rc;
