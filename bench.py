@@ -53,22 +53,38 @@ def parse():
     return ap.parse_args()
 
 
-def stage_bytes(stage, F, W, H, W1, D, ndir, acc):
+def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True):
     """Algorithmic HBM bytes of one step per stage ("Kernels").
 
-    acc = bytes per (pixel, disparity) of the cross-direction delta
-    accumulator (1 when ndir * P2 <= 255, else 2).
+    acc = bytes per (pixel, disparity) of a path-delta accumulator plane (1 when
+    ndir * P2 <= 255, else 2).  strips = the sheared-strip schedule (D in
+    {32, 64, 128, 256}): the strip kernel runs npass passes (down, + up for 8
+    paths) that each read C and write their own plane, the L->R line kernel
+    reads C and writes a plane, the final kernel reads C and every plane.
+    Otherwise one kernel per direction: the first writes the accumulator, the
+    others read and rewrite it, the final kernel reads C and it.
     """
     cells = W1 * H * D
     px = W * H
+    npass = 2 if ndir == 8 else 1
+    if strips:
+        planes = npass + 1
+        strip_b = F * cells * npass * (2 + acc)
+        lines_b = F * cells * (2 + acc)
+        path_b = strip_b + lines_b
+        final_b = F * (cells * (2 + planes * acc) + 2 * px)
+    else:
+        strip_b = lines_b = 0
+        path_b = F * cells * ((2 + acc) + (ndir - 2) * (2 + 2 * acc))
+        final_b = F * (cells * (2 + acc) + 2 * px)
     return {
         "prefilter": F * (2 * px + 2 * 8 * px),
         "cost_volume": F * (2 * 8 * px + 2 * cells),
         "cost_fixup": 0,
-        # first direction: read C, write acc; the others: read C, read + write acc
-        "path_aggregation": F * cells * ((2 + acc) + (ndir - 2) * (2 + 2 * acc)),
-        # last direction + WTA: read C and acc, write the int16 row
-        "final_wta_lr": F * (cells * (2 + acc) + 2 * px),
+        "path_aggregation": path_b,
+        "path_strips": strip_b,
+        "path_lines": lines_b,
+        "final_wta_lr": final_b,
         "post_filters": F * 4 * px,
     }.get(stage, 0)
 
@@ -175,9 +191,13 @@ def main():
         mpix = world * F * W * H * K / elapsed / 1e6
         stages = {k: {"ms_per_step": v[0] / K, "launches_per_step": v[1] / K}
                   for k, v in prof.items() if v[1]}
-        dom = max(stages, key=lambda k: stages[k]["ms_per_step"])
+        strips = D in (32, 64, 128, 256)
+        # dominant KERNEL: path_aggregation is the span of the strip and line
+        # kernels (which run concurrently) when both are timed separately
+        kernels = [k for k in stages if not (k == "path_aggregation" and "path_strips" in stages)]
+        dom = max(kernels, key=lambda k: stages[k]["ms_per_step"])
         launches = stages[dom]["launches_per_step"]
-        bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir, acc) / launches
+        bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir, acc, strips) / launches
         avg_launch_s = stages[dom]["ms_per_step"] / launches / 1e3
         achieved = bytes_per_launch / avg_launch_s / 1e9
         traffic = None

@@ -193,11 +193,13 @@ MVSV_API int mvsv_load_sgbm_yaml(const char* path, mvsv_sgbm_params* p,
  * required. */
 MVSV_API int mvsv_load_bm_yaml(const char* path, mvsv_bm_params* p);
 
-/* Stage profiling with HIP events recorded on the context stream (used by
- * bench.py to time the dominant kernel live).  Stages: 0 prefilter, 1 cost
- * volume, 2 cost fixup, 3 path aggregation (one launch per direction),
- * 4 final direction + WTA/LR, 5 post-filters (median + speckle), 6 BM match. */
-#define MVSV_NUM_STAGES 7
+/* Stage profiling with HIP events (used by bench.py to time the dominant kernel
+ * live).  Stages: 0 prefilter, 1 cost volume, 2 cost fixup, 3 path aggregation
+ * (span of all direction passes before the final one), 4 final direction +
+ * WTA/LR, 5 post-filters (median + speckle), 6 BM match, 7 path strips (the
+ * sheared-strip kernel alone, inside stage 3), 8 path lines (the L->R line
+ * kernel on the second stream, overlapping stage 7). */
+#define MVSV_NUM_STAGES 9
 MVSV_API int mvsv_profile_enable(mvsv_ctx* ctx, int on);
 MVSV_API int mvsv_profile_reset(mvsv_ctx* ctx);
 /* Synchronizes, then writes accumulated milliseconds and launch counts per stage. */

@@ -31,7 +31,7 @@ PREFILTER_XSOBEL = 1
 VARIANT_FIRSTCOL_FIX = 1
 VARIANT_WTA_MIN_D = 2
 
-NUM_STAGES = 7
+NUM_STAGES = 9
 
 _CODES = {
     MVSV_E_INVALID_ARG: "invalid argument",

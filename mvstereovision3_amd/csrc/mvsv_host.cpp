@@ -67,18 +67,18 @@ static hipEvent_t pool_get(mvsv_ctx* ctx)
     return e;
 }
 
-StageTimer::StageTimer(mvsv_ctx* c, int s) : ctx(c), stage(s)
+StageTimer::StageTimer(mvsv_ctx* c, int s, hipStream_t on) : ctx(c), stage(s), st(on ? on : c->stream)
 {
     if (!ctx->prof) return;
     a = pool_get(ctx);
     b = pool_get(ctx);
-    if (a) (void)hipEventRecord(a, ctx->stream);
+    if (a) (void)hipEventRecord(a, st);
 }
 
 StageTimer::~StageTimer()
 {
     if (!ctx->prof || !a || !b) return;
-    (void)hipEventRecord(b, ctx->stream);
+    (void)hipEventRecord(b, st);
     ctx->marks.push_back({stage, a, b});
 }
 
@@ -291,7 +291,7 @@ int mvsv_trim(mvsv_ctx* ctx)
 
 static const char* kStageNames[MVSV_NUM_STAGES] = {
     "prefilter", "cost_volume", "cost_fixup", "path_aggregation", "final_wta_lr", "post_filters",
-    "bm_match"};
+    "bm_match", "path_strips", "path_lines"};
 
 const char* mvsv_profile_stage_name(int s)
 {

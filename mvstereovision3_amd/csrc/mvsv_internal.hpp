@@ -67,6 +67,7 @@ struct mvsv_ctx {
     int path16 = 1;  // 16-lanes-per-scanline path kernels where D allows
     int cost2 = 1;   // register-ring cost kernel where blockSize <= 15
     int tri = 1;     // sheared-strip kernels: three directions per sweep
+    int lines_aux = 0;  // L->R line kernel on the second stream, beside the strip kernel
     // BM
     mvsv::DevBuf bm_lf, bm_rf, bm_cost;
     // host-pointer staging
@@ -87,14 +88,25 @@ int set_error(mvsv_ctx* ctx, int code, const std::string& msg);
 int ensure(mvsv_ctx* ctx, DevBuf& b, size_t bytes, const char* what);
 int check_hip(mvsv_ctx* ctx, hipError_t e, const char* what);
 
-enum Stage { kStagePre = 0, kStageCost, kStageFixup, kStagePath, kStageFinal, kStagePost, kStageBm };
+enum Stage {
+    kStagePre = 0,
+    kStageCost,
+    kStageFixup,
+    kStagePath,
+    kStageFinal,
+    kStagePost,
+    kStageBm,
+    kStageStrips,
+    kStageLines
+};
 // RAII: records a start / stop event pair around the launches in its scope
 // when profiling is enabled (no-op otherwise).
 struct StageTimer {
     mvsv_ctx* ctx;
     int stage;
+    hipStream_t st;  // stream the events are recorded on (default: the context stream)
     hipEvent_t a = nullptr, b = nullptr;
-    StageTimer(mvsv_ctx* c, int s);
+    StageTimer(mvsv_ctx* c, int s, hipStream_t on = nullptr);
     ~StageTimer();
 };
 

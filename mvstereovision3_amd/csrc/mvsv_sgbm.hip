@@ -1045,7 +1045,7 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
 // one extra wave per block does all strip-to-strip traffic, so the compute
 // waves' memory counters only ever wait for their own C loads.
 // ---------------------------------------------------------------------------
-constexpr int kTriWaves = 8;            // compute waves
+constexpr int kTriWaves = 15;           // compute waves
 constexpr int kTriSW = 4 * kTriWaves;  // U-columns per strip
 constexpr int kTriPF = 2;               // steps of C prefetch (compute waves)
 constexpr int kTriBF = 2;               // steps of boundary prefetch (comm wave)
@@ -1248,11 +1248,14 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     };
 
     // ---- compute waves ----
+    // cell (x, y) of step t: y*W1 + x = c0 + t*(sy*W1 + 1), element offsets in
+    // int32 (the launcher checks H*W1*D < 2^31); cells outside the image read
+    // the frame's first cell and store into the lane's dummy slot
     auto cell_x = [&](int t) { return U - (H - 1) + t; };
-    auto cell_off = [&](int t) -> size_t {
-        const int x = clampi(cell_x(t), 0, W1 - 1);
-        const int y = sy > 0 ? t : H - 1 - t;
-        return ((size_t)y * W1 + x) * D;
+    const int c0D = ((sy > 0 ? 0 : (H - 1) * W1) + U - (H - 1)) * D;
+    const int cstepD = (sy * W1 + 1) * D;
+    auto cell_off = [&](int t) -> int {
+        return (unsigned)cell_x(t) < (unsigned)W1 ? c0D + t * cstepD : 0;
     };
     uint32_t la[NP];
 #pragma unroll
@@ -1761,6 +1764,12 @@ __global__ void fill_s16_kernel(int16_t* __restrict__ out, size_t os, size_t ofs
     for (int x = threadIdx.x; x < W; x += blockDim.x) o[x] = v;
 }
 
+// sheared-strip schedule: enabled, and int32 element offsets cover a frame
+static bool use_strips(const mvsv_ctx* ctx, const SgbmEff& e, int H)
+{
+    return ctx->tri && (size_t)H * e.W1 * e.D < ((size_t)1 << 31);
+}
+
 template <int NP, typename AccT>
 int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
                int npass)
@@ -1847,11 +1856,20 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
         if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_fork, s), "fork")) ||
             (rc = check_hip(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0), "fork wait")))
             return rc;
-        dim3 grid((num_lines(1, 0, e.W1, H) + 15) / 16, n);
-        hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT>), grid, dim3(256), 0, ctx->aux, Cv,
-                           Av + npass * plane, dummy, H, e.W1, e.D, 1, 0, e.P1, e.P2);
+        hipStream_t ls = ctx->lines_aux ? ctx->aux : s;
+        auto lines = [&]() {
+            StageTimer tl(ctx, kStageLines, ls);
+            dim3 grid((num_lines(1, 0, e.W1, H) + 15) / 16, n);
+            hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT>), grid, dim3(256), 0, ls, Cv,
+                               Av + npass * plane, dummy, H, e.W1, e.D, 1, 0, e.P1, e.P2);
+        };
+        if (ctx->lines_aux) lines();
         if ((rc = check_hip(ctx, hipGetLastError(), "sgbm L->R lines"))) return rc;
-        if ((rc = launch_tri<NP, AccT>(ctx, n, H, e, Cv, Av, plane, npass))) return rc;
+        {
+            StageTimer ts(ctx, kStageStrips);
+            if ((rc = launch_tri<NP, AccT>(ctx, n, H, e, Cv, Av, plane, npass))) return rc;
+        }
+        if (!ctx->lines_aux) lines();
         if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_join, ctx->aux), "join")) ||
             (rc = check_hip(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0), "join wait")))
             return rc;
@@ -1878,7 +1896,7 @@ int launch_paths16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t
     if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
     AccT* dummy = (AccT*)ctx->dummy.ptr;
     const size_t plane = (size_t)n * H * e.W1 * e.D;
-    if (ctx->tri) return launch_paths_tri<NP, AccT>(ctx, n, H, W, e, Cv, Av, plane, raw);
+    if (use_strips(ctx, e, H)) return launch_paths_tri<NP, AccT>(ctx, n, H, W, e, Cv, Av, plane, raw);
     const int ndir = e.fullDP ? 7 : 4;
     for (int k = 0; k < ndir; k++) {
         int dx = e.fullDP ? dirs_hh[k][0] : dirs_sgbm[k][0];
@@ -2045,7 +2063,7 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     if ((rc = ensure(ctx, ctx->cost, (size_t)n * vol * 2, "sgbm cost volume"))) return rc;
     // accumulator planes: one per concurrently written direction group
     const bool wide16 = ctx->path16 && (e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256);
-    const int nplanes = (wide16 && ctx->tri) ? (e.fullDP ? 3 : 2) : 1;
+    const int nplanes = (wide16 && use_strips(ctx, e, H)) ? (e.fullDP ? 3 : 2) : 1;
     if ((rc = ensure(ctx, ctx->agg, (size_t)nplanes * n * vol * (acc_is_u8(e) ? 1 : 2),
                      "sgbm path-delta accumulator")))
         return rc;

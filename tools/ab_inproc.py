@@ -57,7 +57,6 @@ def main():
                                   ctypes.byref(p), out.data_ptr(), W, W * H)
         assert rc == 0, lib.mvsv_last_error(ctx)
 
-    names = [lib.mvsv_profile_stage_name(i).decode() for i in range(_lib.NUM_STAGES)]
     res = {r[0]: {"total": []} for r in runs}
     for name, lib, ctx, p, out in runs:  # warm-up
         step(lib, ctx, p, out)
@@ -77,7 +76,8 @@ def main():
             cnt = (ctypes.c_int * _lib.NUM_STAGES)()
             lib.mvsv_profile_read(ctx, ms, cnt, _lib.NUM_STAGES)
             res[name]["total"].append(s0.elapsed_time(s1) / a.steps)
-            for i, n in enumerate(names):
+            for i in range(_lib.NUM_STAGES):
+                n = lib.mvsv_profile_stage_name(i).decode() or f"stage{i}"
                 if cnt[i]:
                     res[name].setdefault(n, []).append(ms[i] / a.steps)
     base = outs[libs[0]]

@@ -14,8 +14,9 @@ import json
 import sys
 from collections import defaultdict
 
-STAGES = [("sgbm_path_kernel", "path_aggregation"), ("sgbm_cost_fixup", "cost_fixup"),
-          ("sgbm_cost_kernel", "cost_volume"), ("sgbm_final_kernel", "final_wta_lr"),
+STAGES = [("sgbm_tri_kernel", "path_strips"), ("sgbm_path16_kernel", "path_lines"),
+          ("sgbm_path_kernel", "path_aggregation"), ("sgbm_cost_fixup", "cost_fixup"),
+          ("sgbm_cost", "cost_volume"), ("sgbm_final", "final_wta_lr"),
           ("sgbm_prefilter", "prefilter"), ("median3x3", "post_filters"),
           ("speckle", "post_filters"), ("bm_match", "bm_match")]
 
