@@ -23,6 +23,13 @@
  *   mvsv_mean_disparity_grid_device   MeanDisparityDetection::build(MEAN_VALUE)
  *                                     src/MeanDisparityDetection.cpp:159-206 +
  *                                     Utility::calcMeanDisparity src/utility.cpp:265-285
+ *   mvsv_reproject_device             Utility::calcCoordinate src/utility.cpp:176-198,
+ *                                     per pixel (the loop of Utility::dmap2pcl :242-262)
+ *   mvsv_calc_coordinate / _distance  Utility::calcCoordinate / calcDistance
+ *   / _dmap_values                    src/utility.cpp:176-240 (host, one point)
+ *   mvsv_write_ply                    ply::write src/ply.cpp:37-133 (MODE PLAIN,
+ *                                     WITH_COLOR, WITH_COLOR_SHADING)
+ *   mvsv_dmap2pcl                     Utility::dmap2pcl src/utility.cpp:242-262
  *
  * Conventions
  *   - Plain C types only; no exceptions cross this boundary.
@@ -178,6 +185,46 @@ MVSV_API size_t mvsv_sgbm_workspace_bytes(int n, int width, int height,
 MVSV_API int mvsv_mean_disparity_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap,
                                              size_t stride, size_t frame_stride, int width,
                                              int height, float* means);
+
+/* ---- after the path: reprojection and point-cloud output ----
+ * Q is the 4x4 CV_32F reprojection matrix of stereoRectify, 16 floats row-major
+ * (e.g. afterCalibrationParameters.yml "Q"). */
+
+/* Utility::calcCoordinate for every pixel of n int16 maps (device pointers):
+ * (X, Y, Z, W) = Q * (x, y, v / 16, 1) in OpenCV's float GEMM arithmetic, divided
+ * by W; Z = 0 where Z / 1000 is infinite.  xyzw[f][y][x] = (X, Y, Z, v > 0), i.e.
+ * float4 per pixel, row stride / frame stride in float4 elements. */
+MVSV_API int mvsv_reproject_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t stride,
+                                   size_t frame_stride, int width, int height, const float* Q,
+                                   float* xyzw, size_t xyzw_stride, size_t xyzw_frame_stride);
+
+/* Utility::calcCoordinate (one point, host): out = (X, Y, Z, 1). */
+MVSV_API void mvsv_calc_coordinate(float image_x, float image_y, float d_value, const float* Q,
+                                   float* out4);
+/* Utility::calcDistance: Z / 1000 of calcCoordinate, 0 when infinite. */
+MVSV_API float mvsv_calc_distance(float image_x, float image_y, float d_value, const float* Q);
+/* Utility::calcDMapValues: metric point (x, y, z) -> image x, y and disparity * 16. */
+MVSV_API void mvsv_calc_dmap_values(const float* c3, const float* Q, float* image_x,
+                                    float* image_y, float* d_value);
+
+enum { MVSV_PLY_PLAIN = 0, MVSV_PLY_WITH_COLOR = 1, MVSV_PLY_WITH_COLOR_SHADING = 2 };
+
+/* ply::write: ASCII PLY of count vertices (x, y, z floats, vertex_stride floats
+ * apart).  WITH_COLOR greys each vertex by (z - min) / (max - min) * 255 with the
+ * min / max of the positive values of the int16 map dmap (the ply's mDMap);
+ * WITH_COLOR_SHADING declares colour properties but writes none (as the
+ * reference does).  Colour modes need dmap (returns MVSV_E_INVALID_ARG if it is
+ * empty or has no positive value).  Host-only; MVSV_E_IO if the file cannot be
+ * opened. */
+MVSV_API int mvsv_write_ply(const char* path, const char* author, const char* object_name,
+                            const float* xyz, size_t count, size_t vertex_stride, int mode,
+                            const int16_t* dmap, size_t dmap_stride, int width, int height);
+
+/* Utility::dmap2pcl: every pixel of the host int16 map with v > 0 reprojected
+ * (on the device of ctx) and written as "Hagen Hiller" / "disparity pointcloud"
+ * PLY in MODE WITH_COLOR, raster order. */
+MVSV_API int mvsv_dmap2pcl(mvsv_ctx* ctx, const char* path, const int16_t* dmap, size_t stride,
+                           int width, int height, const float* Q);
 
 /* Disparity::loadSGBMParameters: reads configs/sgbm.yml keys minDisp, numDisp,
  * blockSize, disp12MaxDiff, preFilterCap, uniquenessRatio, speckleWindowSize,

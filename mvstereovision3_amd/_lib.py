@@ -115,6 +115,13 @@ def _declare(lib):
         "mvsv_profile_reset": ([P], I),
         "mvsv_profile_read": ([P, P, P, I], I),
         "mvsv_profile_stage_name": ([I], ctypes.c_char_p),
+        "mvsv_reproject_device": ([P, I, P, Z, Z, I, I, P, P, Z, Z], I),
+        "mvsv_calc_coordinate": ([ctypes.c_float] * 3 + [P, P], None),
+        "mvsv_calc_distance": ([ctypes.c_float] * 3 + [P], ctypes.c_float),
+        "mvsv_calc_dmap_values": ([P, P, P, P, P], None),
+        "mvsv_write_ply": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, P, Z, Z, I, P, Z,
+                            I, I], I),
+        "mvsv_dmap2pcl": ([P, ctypes.c_char_p, P, Z, I, I, P], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

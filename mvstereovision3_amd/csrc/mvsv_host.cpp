@@ -651,3 +651,147 @@ int mvsv_synth_pair(uint32_t seed, int W, int H, int minD, int D, uint8_t* Lout,
 }
 
 }  // extern "C"
+
+// ---- reprojection and PLY output -------------------------
+
+int mvsv_reproject_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_t fs, int W,
+                          int H, const float* Q, float* xyzw, size_t xs, size_t xfs)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    if (n <= 0 || !dmap || !Q || !xyzw || W <= 0 || H <= 0 || st < (size_t)W || xs < (size_t)W)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "bad reprojection arguments");
+    (void)hipSetDevice(ctx->device);
+    return reproject_device(ctx, n, dmap, st, fs, W, H, Q, xyzw, xs, xfs);
+}
+
+// [Utility::calcCoordinate] src/utility.cpp:176-198 with OpenCV's float matrix
+// product (double accumulation, one rounding) and Mat /= w (float scale).
+void mvsv_calc_coordinate(float image_x, float image_y, float d_value, const float* Q, float* out)
+{
+    const float c[4] = {image_x, image_y, d_value / 16, 1.0f};
+    float r[4];
+    for (int i = 0; i < 4; i++) {
+        double acc = 0.0;
+        for (int k = 0; k < 4; k++) acc += (double)Q[4 * i + k] * (double)c[k];
+        r[i] = (float)acc;
+    }
+    const float alpha = (float)(1.0 / (double)r[3]);
+    for (int i = 0; i < 4; i++) out[i] = r[i] * alpha;
+    if (std::isinf(out[2] / 1000)) out[2] = 0.0f;
+}
+
+// [Utility::calcDistance] src/utility.cpp:200-222
+float mvsv_calc_distance(float image_x, float image_y, float d_value, const float* Q)
+{
+    const float c[4] = {image_x, image_y, d_value / 16, 1.0f};
+    float r[4];
+    for (int i = 0; i < 4; i++) {
+        double acc = 0.0;
+        for (int k = 0; k < 4; k++) acc += (double)Q[4 * i + k] * (double)c[k];
+        r[i] = (float)acc;
+    }
+    const float alpha = (float)(1.0 / (double)r[3]);
+    const float distance = (r[2] * alpha) / 1000;
+    return std::isinf(distance) ? 0.0f : distance;
+}
+
+// [Utility::calcDMapValues] src/utility.cpp:224-240
+void mvsv_calc_dmap_values(const float* c, const float* Q, float* image_x, float* image_y,
+                           float* d_value)
+{
+    const float numerator = Q[2 * 4 + 3] - c[2] * Q[3 * 4 + 3];
+    const float denominator = c[2] * Q[3 * 4 + 2];
+    const float disparity_value = numerator / denominator;
+    *image_x = c[0] * (disparity_value * Q[3 * 4 + 2] * Q[3 * 4 + 3]) + Q[0 * 4 + 3];
+    *image_y = c[1] * (disparity_value * Q[3 * 4 + 2] * Q[3 * 4 + 3]) + Q[1 * 4 + 3];
+    *d_value = disparity_value * 16;
+}
+
+// [Utility::calcMinMaxDisparity] src/utility.cpp:286-303 (positive values only)
+static bool min_max_positive(const int16_t* d, size_t st, int W, int H, short* mn, short* mx)
+{
+    bool any = false;
+    for (int r = 0; r < H; r++)
+        for (int c = 0; c < W; c++) {
+            const short v = d[(size_t)r * st + c];
+            if (v > 0) {
+                if (!any || v < *mn) *mn = v;
+                if (!any || v > *mx) *mx = v;
+                any = true;
+            }
+        }
+    return any;
+}
+
+// [ply::write] src/ply.cpp:37-133: std::ofstream with default float formatting
+int mvsv_write_ply(const char* path, const char* author, const char* object_name,
+                   const float* xyz, size_t count, size_t vstride, int mode, const int16_t* dmap,
+                   size_t dst, int W, int H)
+{
+    if (!path || (!xyz && count) || vstride < 3 || mode < MVSV_PLY_PLAIN ||
+        mode > MVSV_PLY_WITH_COLOR_SHADING)
+        return MVSV_E_INVALID_ARG;
+    short mn = 0, mx = 0;
+    if (mode != MVSV_PLY_PLAIN) {
+        if (!dmap || W <= 0 || H <= 0) return MVSV_E_INVALID_ARG;  // "mDMap.rows == 0" -> false
+        if (!min_max_positive(dmap, dst, W, H, &mn, &mx)) return MVSV_E_INVALID_ARG;
+    }
+    std::ofstream out(path);
+    if (!out) return MVSV_E_IO;
+    out << "ply\nformat ascii 1.0\ncomment author: " << (author ? author : "")
+        << "\ncomment object:" << (object_name ? object_name : "") << "\n";
+    out << "element vertex " << std::to_string(count) << "\n";
+    out << "property float x\nproperty float y\nproperty float z\n";
+    if (mode != MVSV_PLY_PLAIN) out << "property uchar red\nproperty uchar green\nproperty uchar blue\n";
+    out << "end_header\n";
+    for (size_t i = 0; i < count; i++) {
+        const float* t = xyz + i * vstride;
+        if (mode == MVSV_PLY_WITH_COLOR) {
+            out << t[0] << " " << t[1] << " " << t[2] << " ";
+            const int g = int((t[2] - mn) / (mx - mn) * 255.0);
+            out << g << " " << g << " " << g << "\n";
+        } else {
+            out << t[0] << " " << t[1] << " " << t[2] << "\n";
+        }
+    }
+    return out ? MVSV_OK : MVSV_E_IO;
+}
+
+// [Utility::dmap2pcl] src/utility.cpp:242-262
+int mvsv_dmap2pcl(mvsv_ctx* ctx, const char* path, const int16_t* dmap, size_t st, int W, int H,
+                  const float* Q)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    if (!path || !dmap || !Q || W <= 0 || H <= 0 || st < (size_t)W)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "bad dmap2pcl arguments");
+    (void)hipSetDevice(ctx->device);
+    const size_t px = (size_t)W * H;
+    int rc;
+    if ((rc = ensure(ctx, ctx->h_out, px * 2, "dmap staging"))) return rc;
+    if ((rc = ensure(ctx, ctx->h_left, px * 16, "point staging"))) return rc;
+    hipStream_t s = ctx->stream;
+    if ((rc = check_hip(ctx, hipMemcpy2DAsync(ctx->h_out.ptr, (size_t)W * 2, dmap, st * 2,
+                                              (size_t)W * 2, H, hipMemcpyHostToDevice, s),
+                        "H2D dmap")))
+        return rc;
+    if ((rc = reproject_device(ctx, 1, (const int16_t*)ctx->h_out.ptr, W, px, W, H, Q,
+                               (float*)ctx->h_left.ptr, W, px)))
+        return rc;
+    std::vector<float> pts(px * 4);
+    if ((rc = check_hip(ctx, hipMemcpyAsync(pts.data(), ctx->h_left.ptr, px * 16,
+                                            hipMemcpyDeviceToHost, s),
+                        "D2H points")) ||
+        (rc = check_hip(ctx, hipStreamSynchronize(s), "hipStreamSynchronize")))
+        return rc;
+    size_t k = 0;
+    for (size_t i = 0; i < px; i++)  // raster order, v > 0 (flag in the 4th float)
+        if (pts[4 * i + 3] != 0.0f) {
+            for (int j = 0; j < 4; j++) pts[4 * k + j] = pts[4 * i + j];
+            k++;
+        }
+    rc = mvsv_write_ply(path, "Hagen Hiller", "disparity pointcloud", pts.data(), k, 4,
+                        MVSV_PLY_WITH_COLOR, dmap, st, W, H);
+    if (rc == MVSV_E_IO) return set_error(ctx, rc, std::string("cannot write ") + path);
+    if (rc) return set_error(ctx, rc, "dmap2pcl: map has no positive disparity");
+    return MVSV_OK;
+}

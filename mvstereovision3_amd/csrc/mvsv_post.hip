@@ -339,6 +339,40 @@ __global__ __launch_bounds__(256) void mean_grid_kernel(const int16_t* __restric
     }
 }
 
+// ---- Utility::calcCoordinate per pixel (src/utility.cpp:176-198) -------------
+// (X, Y, Z, W) = Q * (x, y, v / 16, 1) with OpenCV's float GEMM (products and
+// sums in double, one rounding to float per element), then Mat /= W as
+// convertTo(alpha = (float)(1 / W)) (float multiply); Z = 0 when Z / 1000 is
+// infinite.  The 4th output is 1 for v > 0 (the pixels Utility::dmap2pcl keeps).
+struct QMat {
+    float q[16];
+};
+
+__global__ __launch_bounds__(256) void reproject_kernel(const int16_t* __restrict__ dmap, size_t st,
+                                                        size_t fs, int W, int H, QMat Q,
+                                                        float4* __restrict__ out, size_t os,
+                                                        size_t ofs)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.z;
+    if (x >= W || y >= H) return;
+    const float v = (float)dmap[f * fs + (size_t)y * st + x];
+    const float c[4] = {(float)x, (float)y, v / 16.0f, 1.0f};
+    float r[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) acc = __dadd_rn(acc, __dmul_rn((double)Q.q[4 * i + k], (double)c[k]));
+        r[i] = (float)acc;
+    }
+    const float alpha = (float)(1.0 / (double)r[3]);
+    float X = __fmul_rn(r[0], alpha), Y = __fmul_rn(r[1], alpha), Z = __fmul_rn(r[2], alpha);
+    if (isinf(__fdiv_rn(Z, 1000.0f))) Z = 0.0f;
+    out[f * ofs + (size_t)y * os + x] = make_float4(X, Y, Z, v > 0.0f ? 1.0f : 0.0f);
+}
+
 }  // namespace
 
 int median3x3_device(mvsv_ctx* ctx, int n, const int16_t* src, size_t ss, size_t sfs, int16_t* dst,
@@ -382,6 +416,17 @@ int mean_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_
     hipLaunchKernelGGL(mean_grid_kernel, dim3(81, n), dim3(256), 0, ctx->stream, dmap, st, fs, W,
                        H, means);
     return check_hip(ctx, hipGetLastError(), "mean disparity grid");
+}
+
+int reproject_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_t fs, int W, int H,
+                     const float* Q, float* out, size_t os, size_t ofs)
+{
+    QMat q;
+    for (int i = 0; i < 16; i++) q.q[i] = Q[i];
+    dim3 grid((W + 63) / 64, (H + 3) / 4, n);
+    hipLaunchKernelGGL(reproject_kernel, grid, dim3(256), 0, ctx->stream, dmap, st, fs, W, H, q,
+                       (float4*)out, os, ofs);
+    return check_hip(ctx, hipGetLastError(), "reprojection");
 }
 
 }  // namespace mvsv

@@ -13,6 +13,7 @@
 #include "mvsv_oracle.h"
 
 #include <limits.h>
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -830,5 +831,29 @@ void orc_mean_disparity_grid(const int16_t* dmap, ptrdiff_t st, int W, int H, fl
                     if (v > 1) { total += v; n++; }
                 }
             means[r * 9 + c] = (total == 0 || n == 0) ? 0.0f : (float)(total / iabs(n));
+        }
+}
+
+/* [Utility::calcCoordinate] src/utility.cpp:176-198, applied per pixel as in
+ * Utility::dmap2pcl src/utility.cpp:242-262 */
+void orc_reproject(const int16_t* dmap, ptrdiff_t st, int W, int H, const float* Q, float* out)
+{
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            float v = (float)dmap[(ptrdiff_t)y * st + x];
+            float c[4] = {(float)x, (float)y, v / 16, 1.0f};
+            float r[4];
+            for (int i = 0; i < 4; i++) {
+                double acc = 0.0;
+                for (int k = 0; k < 4; k++) acc += (double)Q[4 * i + k] * (double)c[k];
+                r[i] = (float)acc;
+            }
+            float alpha = (float)(1.0 / (double)r[3]);
+            float* o = out + ((size_t)y * W + x) * 4;
+            o[0] = r[0] * alpha;
+            o[1] = r[1] * alpha;
+            o[2] = r[2] * alpha;
+            if (isinf(o[2] / 1000)) o[2] = 0.0f;
+            o[3] = v > 0 ? 1.0f : 0.0f;
         }
 }

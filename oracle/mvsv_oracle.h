@@ -94,6 +94,13 @@ int orc_filter_speckles_s16(int16_t* img, ptrdiff_t stride, int W, int H,
 /* MeanDisparityDetection::build(MEAN_VALUE) post-pass: 81 tile means over a
  * CV_16S map (src/MeanDisparityDetection.cpp:159-206, Utility::
  * calcMeanDisparity src/utility.cpp:265-285). means[81] row-major tiles. */
+/* Utility::calcCoordinate (src/utility.cpp:176-198) for every pixel:
+ * out[y][x] = (X, Y, Z, v > 0), Q 4x4 CV_32F row-major.  OpenCV float Mat
+ * product (double accumulation over k = 0..3, one rounding), then Mat /= W
+ * (convertTo with float alpha = 1 / W), Z = 0 when Z / 1000 is infinite. */
+void orc_reproject(const int16_t* dmap, ptrdiff_t stride, int W, int H, const float* Q,
+                   float* out);
+
 void orc_mean_disparity_grid(const int16_t* dmap, ptrdiff_t stride, int W,
                              int H, float* means);
 

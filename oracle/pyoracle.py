@@ -62,6 +62,7 @@ def lib():
         _lib.orc_filter_speckles_s16.argtypes = [P, S, I, I, I, I, I]
         _lib.orc_filter_speckles_s16.restype = I
         _lib.orc_mean_disparity_grid.argtypes = [P, S, I, I, P]
+        _lib.orc_reproject.argtypes = [P, S, I, I, P, P]
     return _lib
 
 
@@ -149,4 +150,14 @@ def mean_disparity_grid(d) -> np.ndarray:
     H, W = d.shape
     out = np.zeros(81, np.float32)
     lib().orc_mean_disparity_grid(_ptr(d), W, W, H, _ptr(out))
+    return out
+
+
+def reproject(dmap: np.ndarray, Q) -> np.ndarray:
+    """Utility::calcCoordinate per pixel -> (H, W, 4) float32 (X, Y, Z, valid)."""
+    d = np.ascontiguousarray(dmap, np.int16)
+    H, W = d.shape
+    q = np.ascontiguousarray(np.asarray(Q, np.float32).reshape(16))
+    out = np.empty((H, W, 4), np.float32)
+    lib().orc_reproject(_ptr(d), W, W, H, _ptr(q), _ptr(out))
     return out

@@ -325,3 +325,39 @@ def test_size_independent_properties_full_batch(gpu, mvsv):
     assert (a[valid] >= 16).all() and (a[valid] <= 128 * 16 + 16).all()
     # the rectangle of the synthetic field sits at round(0.6 * D) = 77
     assert abs(np.median(a[:, 400:560, 500:800]) / 16 - 77) < 1
+
+
+# -------------------------------------------------- after the path (f3/f4) -----
+def test_reproject_matches_oracle(gpu, mvsv, oracle):
+    import json
+    import os
+    import torch
+    from conftest import GOLDEN
+    from mvstereovision3_amd.utility import reproject
+    Q = np.array(json.load(open(os.path.join(GOLDEN, "q_matrix.json")))["Q"], np.float32)
+    L, R = mvsv.synth_pair(SEED0 + 5, 400, 120, 0, 64)
+    d = mvsv.StereoSGBM.create(0, 64, 5).compute(L, R)
+    d[0, :5] = 0  # W = 0 -> infinite Z -> 0
+    d[1, :5] = -16
+    got = reproject(torch.from_numpy(d).cuda(), Q).cpu().numpy()
+    want = oracle.reproject(d, Q)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    batch = torch.from_numpy(np.stack([d, d[::-1].copy()])).cuda()
+    gb = reproject(batch, Q).cpu().numpy()
+    assert np.array_equal(gb[1].view(np.uint32), oracle.reproject(d[::-1].copy(), Q).view(np.uint32))
+
+
+def test_dmap2pcl_writes_reference_ply(gpu, mvsv, oracle, tmp_path):
+    import json
+    import os
+    from conftest import GOLDEN
+    from test_utility import ply_text
+    from mvstereovision3_amd.utility import Utility
+    Q = np.array(json.load(open(os.path.join(GOLDEN, "q_matrix.json")))["Q"], np.float32)
+    L, R = mvsv.synth_pair(SEED0 + 6, 200, 60, 0, 32)
+    d = mvsv.StereoSGBM.create(0, 32, 5).compute(L, R)
+    f = tmp_path / "cloud.ply"
+    Utility.dmap2pcl(str(f), d, Q)
+    pts = oracle.reproject(d, Q).reshape(-1, 4)
+    pts = pts[pts[:, 3] > 0]
+    assert f.read_text() == ply_text(pts, 1, "Hagen Hiller", "disparity pointcloud", d)
