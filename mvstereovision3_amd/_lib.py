@@ -83,7 +83,7 @@ _lib = None
 _lock = threading.Lock()
 
 
-def _declare(lib):
+def _declare(lib, strict=True):
     P = ctypes.c_void_p
     I = ctypes.c_int
     Z = ctypes.c_size_t
@@ -124,7 +124,9 @@ def _declare(lib):
         "mvsv_dmap2pcl": ([P, ctypes.c_char_p, P, Z, I, I, P], I),
     }
     for name, (args, res) in sig.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None) if not strict else getattr(lib, name)
+        if fn is None:  # older A/B builds (strict=False) may lack newer entry points
+            continue
         fn.argtypes = args
         fn.restype = res
     return lib

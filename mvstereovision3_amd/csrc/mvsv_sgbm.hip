@@ -1048,8 +1048,8 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
 constexpr int kTriWaves = 15;           // compute waves
 constexpr int kTriSW = 4 * kTriWaves;  // U-columns per strip
 constexpr int kTriPF = 2;               // steps of C prefetch (compute waves)
-constexpr int kTriBF = 2;               // steps of boundary prefetch (comm wave)
-constexpr int kTriUnroll = 2;           // lcm(kTriPF, kTriBF, 2)
+constexpr int kTriBF = 4;               // steps of boundary prefetch (comm wave)
+constexpr int kTriUnroll = 4;           // lcm(kTriPF, kTriBF, 2)
 constexpr unsigned kTriSpinLimit = 1u << 16;
 
 template <int NP>

@@ -43,7 +43,7 @@ def main():
     outs = {}
     runs = []
     for path in libs:
-        lib = _lib._declare(ctypes.CDLL(path, mode=os.RTLD_LOCAL))
+        lib = _lib._declare(ctypes.CDLL(path, mode=os.RTLD_LOCAL), strict=False)
         ctx = ctypes.c_void_p()
         assert lib.mvsv_create(ctypes.byref(ctx), 0) == 0
         lib.mvsv_set_stream(ctx, None)
