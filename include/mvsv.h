@@ -23,6 +23,11 @@
  *   mvsv_mean_disparity_grid_device   MeanDisparityDetection::build(MEAN_VALUE)
  *                                     src/MeanDisparityDetection.cpp:159-206 +
  *                                     Utility::calcMeanDisparity src/utility.cpp:265-285
+ *   mvsv_mean_disparity_grid          same, host map (MeanDisparityDetection::build)
+ *   mvsv_stream_*                     the disparity worker thread + main loop of
+ *                                     trgt/mean_test.cpp:61-70,258-318 (condvar
+ *                                     hand-off, Disparity::sgbm, build(MEAN_VALUE))
+ *                                     as a double-buffered device pipeline
  *   mvsv_reproject_device             Utility::calcCoordinate src/utility.cpp:176-198,
  *                                     per pixel (the loop of Utility::dmap2pcl :242-262)
  *   mvsv_calc_coordinate / _distance  Utility::calcCoordinate / calcDistance
@@ -185,6 +190,32 @@ MVSV_API size_t mvsv_sgbm_workspace_bytes(int n, int width, int height,
 MVSV_API int mvsv_mean_disparity_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap,
                                              size_t stride, size_t frame_stride, int width,
                                              int height, float* means);
+
+/* Same grid for a host map (synchronous). means: 81 floats, row-major 9x9. */
+MVSV_API int mvsv_mean_disparity_grid(mvsv_ctx* ctx, const int16_t* dmap, size_t stride,
+                                      int width, int height, float* means);
+
+/* ---- frame stream ------------------------------------------
+ * A camera loop pushes rectified pairs from host memory and pops int16 maps in
+ * push order.  Up to `depth` frames are in flight: the upload of one frame, the
+ * SGBM of the previous one (on the context stream) and the download of the one
+ * before overlap.  With grid_roi, each frame's 9x9 MeanDisparityDetection grid
+ * over that ROI of the map (createDMapROIS, trgt/mean_test.cpp:80-106) is
+ * computed on the device and returned by pop. */
+typedef struct mvsv_stream mvsv_stream;
+typedef struct { int x0, y0, x1, y1; } mvsv_rect; /* half-open [x0,x1) x [y0,y1) */
+MVSV_API int mvsv_stream_create(mvsv_ctx* ctx, int width, int height, const mvsv_sgbm_params* p,
+                                int depth, const mvsv_rect* grid_roi, mvsv_stream** out);
+/* new parameters for frames pushed from now on (the reference's setters between frames) */
+MVSV_API int mvsv_stream_set_params(mvsv_stream* s, const mvsv_sgbm_params* p);
+/* MVSV_E_INVALID_ARG when depth frames are already pending (pop first) */
+MVSV_API int mvsv_stream_push(mvsv_stream* s, const uint8_t* left, size_t left_stride,
+                              const uint8_t* right, size_t right_stride);
+/* waits for the oldest pending frame; out (int16, stride in elements) and means
+ * (81 floats) may be NULL */
+MVSV_API int mvsv_stream_pop(mvsv_stream* s, int16_t* out, size_t out_stride, float* means);
+MVSV_API int mvsv_stream_pending(const mvsv_stream* s);
+MVSV_API void mvsv_stream_destroy(mvsv_stream* s);
 
 /* ---- after the path: reprojection and point-cloud output ----
  * Q is the 4x4 CV_32F reprojection matrix of stereoRectify, 16 floats row-major

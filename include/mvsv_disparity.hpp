@@ -179,6 +179,7 @@ public:
     int getP2() const { return p.p2; }
     void setMode(int v) { p.mode = v; }
     int getMode() const { return p.mode; }
+    const mvsv_sgbm_params& params() const { return p; }
     mvsv_sgbm_params p{};
 };
 

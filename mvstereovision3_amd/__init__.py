@@ -10,10 +10,14 @@ from ._lib import (MODE_HH, MODE_SGBM, PREFILTER_NORMALIZED_RESPONSE, PREFILTER_
                    VARIANT_FIRSTCOL_FIX, VARIANT_WTA_MIN_D, MvsvError)
 from .disparity import (Disparity, StereoBM, StereoSGBM, Stereopair, mean_disparity_grid,
                         sgbmParameters, synth_pair)
+from .detection import DisparityStream, MeanDisparityDetection, Subimage, create_dmap_rois
+from .utility import Utility, dMapValues, ply, reproject
 
 __all__ = [
     "Disparity", "StereoBM", "StereoSGBM", "Stereopair", "sgbmParameters", "MvsvError",
     "synth_pair", "mean_disparity_grid", "MODE_SGBM", "MODE_HH", "PREFILTER_XSOBEL",
     "PREFILTER_NORMALIZED_RESPONSE", "VARIANT_FIRSTCOL_FIX", "VARIANT_WTA_MIN_D",
+    "DisparityStream", "MeanDisparityDetection", "Subimage", "create_dmap_rois", "Utility",
+    "dMapValues", "ply", "reproject",
 ]
 __version__ = "1.0.0"

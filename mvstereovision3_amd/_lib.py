@@ -75,6 +75,12 @@ class BmParams(ctypes.Structure):
         return {f: int(getattr(self, f)) for f in BM_FIELDS}
 
 
+class Rect(ctypes.Structure):
+    """mvsv_rect: half-open [x0, x1) x [y0, y1)."""
+    _fields_ = [("x0", ctypes.c_int), ("y0", ctypes.c_int), ("x1", ctypes.c_int),
+                ("y1", ctypes.c_int)]
+
+
 class SgbmYamlValues(ctypes.Structure):
     _fields_ = [(f, ctypes.c_int) for f in YAML_FIELDS]
 
@@ -115,6 +121,13 @@ def _declare(lib, strict=True):
         "mvsv_profile_reset": ([P], I),
         "mvsv_profile_read": ([P, P, P, I], I),
         "mvsv_profile_stage_name": ([I], ctypes.c_char_p),
+        "mvsv_mean_disparity_grid": ([P, P, Z, I, I, P], I),
+        "mvsv_stream_create": ([P, I, I, P, I, P, ctypes.POINTER(P)], I),
+        "mvsv_stream_set_params": ([P, P], I),
+        "mvsv_stream_push": ([P, P, Z, P, Z], I),
+        "mvsv_stream_pop": ([P, P, Z, P], I),
+        "mvsv_stream_pending": ([P], I),
+        "mvsv_stream_destroy": ([P], None),
         "mvsv_reproject_device": ([P, I, P, Z, Z, I, I, P, P, Z, Z], I),
         "mvsv_calc_coordinate": ([ctypes.c_float] * 3 + [P, P], None),
         "mvsv_calc_distance": ([ctypes.c_float] * 3 + [P], ctypes.c_float),

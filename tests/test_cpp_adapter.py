@@ -46,3 +46,30 @@ def test_cpp_adapter_gpu(adapter_bin, tmp_path, gpu, oracle):
     assert np.array_equal(d1, oracle.sgbm(L, R, p))
     b = mvsv.StereoBM.create(64, 9).params()
     assert np.array_equal(d2, oracle.bm(L, R, b))
+
+
+@pytest.fixture(scope="module")
+def detection_bin(tmp_path_factory):
+    from mvstereovision3_amd import _lib
+    _lib.lib()
+    out = str(tmp_path_factory.mktemp("cppdet") / "detection_check")
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-Wno-implicit-fallthrough",
+                    "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "detection_check.cpp"),
+                    "-L", libdir, "-lmvsv", f"-Wl,-rpath,{libdir}", "-o", out], check=True)
+    return out
+
+
+def test_cpp_detection_cpu(detection_bin, tmp_path):
+    r = subprocess.run([detection_bin, "cpu", str(tmp_path)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "cpu ok" in r.stdout
+    assert (tmp_path / "two.ply").read_text().startswith("ply\nformat ascii 1.0\ncomment author: Hagen Hiller")
+
+
+@pytest.mark.gpu
+def test_cpp_detection_gpu(detection_bin, tmp_path, gpu):
+    r = subprocess.run([detection_bin, "gpu", str(tmp_path)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "gpu ok" in r.stdout and (tmp_path / "cloud.ply").exists()

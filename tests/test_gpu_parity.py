@@ -361,3 +361,43 @@ def test_dmap2pcl_writes_reference_ply(gpu, mvsv, oracle, tmp_path):
     pts = oracle.reproject(d, Q).reshape(-1, 4)
     pts = pts[pts[:, 3] > 0]
     assert f.read_text() == ply_text(pts, 1, "Hagen Hiller", "disparity pointcloud", d)
+
+
+# ------------------------------------------------------- f1: stream + grid -----
+def test_mean_grid_host_map(gpu, mvsv, oracle):
+    rng = np.random.default_rng(5)
+    d = rng.integers(-16, 3000, (123, 377)).astype(np.int16)
+    m = mvsv.MeanDisparityDetection()
+    m.init(d.shape, np.eye(4, dtype=np.float32).reshape(16), 0.1, 1.5)
+    m.build(d, 0, m.MEAN_VALUE)
+    assert np.array_equal(np.array(m.getMeanMap(), np.float32), oracle.mean_disparity_grid(d))
+
+
+def test_disparity_stream_matches_direct_compute(gpu, mvsv, oracle):
+    """Camera loop (trgt/mean_test.cpp:61-70, 258-318) as a depth-3 stream with the ROI grid."""
+    W, H = 320, 96
+    m = mvsv.StereoSGBM.create(0, 64, 9, 8 * 81, 32 * 81)  # liveDisparity-style parameters
+    roi_u, _ = mvsv.create_dmap_rois((H, W), 64)
+    st = mvsv.DisparityStream(m, W, H, depth=3, grid_roi=roi_u)
+    frames = [mvsv.synth_pair(SEED0 + 40 + i, W, H, 0, 64) for i in range(7)]
+    got = []
+    for i, (L, R) in enumerate(frames):
+        if st.pending() == 3:
+            got.append(st.pop())
+        if i == 5:  # setters between frames apply to frames pushed afterwards
+            m.setUniquenessRatio(15)
+            st.set_params(m)
+        st.push(L, R)
+    while st.pending():
+        got.append(st.pop())
+    st.close()
+    assert len(got) == 7
+    for i, ((L, R), (d, means)) in enumerate(zip(frames, got)):
+        p = dict(m.params())
+        p.pop("variant")
+        if i < 5:
+            p["uniqueness_ratio"] = 0
+        want = oracle.sgbm(L, R, p)
+        assert np.array_equal(d, want), f"frame {i}: " + report(d, want)
+        x0, y0, x1, y1 = roi_u
+        assert np.array_equal(means, oracle.mean_disparity_grid(np.ascontiguousarray(want[y0:y1, x0:x1])))
