@@ -1045,8 +1045,14 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
 // one extra wave per block does all strip-to-strip traffic, so the compute
 // waves' memory counters only ever wait for their own C loads.
 // ---------------------------------------------------------------------------
-constexpr int kTriWaves = 15;           // compute waves
-constexpr int kTriSW = 4 * kTriWaves;  // U-columns per strip
+// compute waves per block: 15 (+ the exchange wave = 1024 threads, <= 128 VGPRs)
+// for up to 8 disparities per lane; 7 for D = 256 (16 per lane, ~200 VGPRs)
+template <int NP>
+struct TriCfg {
+    static constexpr int kWaves = NP >= 8 ? 7 : 15;
+    static constexpr int kSW = 4 * kWaves;  // U-columns per strip
+    static constexpr int kThreads = 64 * (kWaves + 1);
+};
 constexpr int kTriPF = 2;               // steps of C prefetch (compute waves)
 constexpr int kTriBF = 4;               // steps of boundary prefetch (comm wave)
 constexpr int kTriUnroll = 4;           // lcm(kTriPF, kTriBF, 2)
@@ -1054,7 +1060,7 @@ constexpr unsigned kTriSpinLimit = 1u << 16;
 
 template <int NP>
 struct TriLayout {
-    static constexpr int kCols = kTriSW + 2;           // + two columns of the right strip
+    static constexpr int kCols = TriCfg<NP>::kSW + 2;  // + two columns of the right strip
     static constexpr int kColDw = 16 * NP;              // dwords per column
     static constexpr int kBufDw = 2 * kCols * kColDw;   // dirs b and c
     static constexpr int kLDw = 2 * kBufDw;             // double-buffered
@@ -1110,7 +1116,7 @@ __device__ __forceinline__ size_t tri_slot(int chain, int k, int t, int nchains,
 }
 
 template <int NP, typename AccT>
-__global__ __launch_bounds__(64 * (kTriWaves + 1))
+__global__ __launch_bounds__(TriCfg<NP>::kThreads)
 __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     const int16_t* __restrict__ C, AccT* __restrict__ A, size_t plane, AccT* __restrict__ dummy,
     int H, int W1, int D, int npass, int P1, int P2, unsigned long long* __restrict__ bnd,
@@ -1121,6 +1127,8 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     using TL = TriLayout<NP>;
     using TG = TriGran<NP>;
     constexpr int NG = TG::NG;
+    constexpr int kTriWaves = TriCfg<NP>::kWaves;
+    constexpr int kTriSW = TriCfg<NP>::kSW;
     constexpr int PF = kTriPF;
     constexpr int BF = kTriBF;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1775,6 +1783,7 @@ int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT*
                int npass)
 {
     using TL = TriLayout<NP>;
+    constexpr int kTriSW = TriCfg<NP>::kSW;
     const int nstrips = (e.W1 + H - 1 + kTriSW - 1) / kTriSW;
     const size_t bytes = (size_t)npass * n * nstrips * H * 4 * 16 * TriGran<NP>::NG * 8;
     int rc;
@@ -1799,7 +1808,7 @@ int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT*
         (void)hipMalloc(&stats, (size_t)grid.x * 64);
         (void)hipMemset(stats, 0, (size_t)grid.x * 64);
     }
-    hipLaunchKernelGGL((sgbm_tri_kernel<NP, AccT>), grid, dim3(64 * (kTriWaves + 1)), TL::kBytes,
+    hipLaunchKernelGGL((sgbm_tri_kernel<NP, AccT>), grid, dim3(TriCfg<NP>::kThreads), TL::kBytes,
                        ctx->stream, Cv, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, npass, e.P1,
                        e.P2, (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips,
                        (int*)ctx->status.ptr, stats);

@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""BASELINE config 5: a camera-loop stream through the frame pipeline.
+
+liveDisparity-style matcher create(0, 256, 9, 8*81, 32*81) (MODE_SGBM, no speckle)
+on 1280x960 synthetic rectified pairs, followed by MeanDisparityDetection
+(build(MEAN_VALUE) on the createDMapROIS work ROI x in [128, W), detectObstacles)
+per frame -- the loop of trgt/mean_test.cpp:258-318 without its worker thread.
+Host frames go in, int16 maps and the 81 tile means come back (PCIe included);
+`depth` frames are in flight.  Also reports the device-resident rate of the same
+matcher on a batch of 8 frames.  Not the headline metric (bench.py is).
+
+    python tools/bench_stream.py [--frames 300] [--depth 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=300)
+    ap.add_argument("--depth", type=int, default=3)
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=960)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import mvstereovision3_amd as mvsv
+
+    W, H, D = a.width, a.height, 256
+    m = mvsv.StereoSGBM.create(0, D, 9, 8 * 81, 32 * 81)  # trgt/liveDisparity.cpp:61
+    q = json.load(open(os.path.join(ROOT, "tests", "golden", "q_matrix.json")))["Q"]
+    Q = np.array(q, np.float32).reshape(4, 4)
+    Q[0, 3] *= 2  # afterCalibrationParameters.yml is for 752x480: x2 for 1280x960-class sensors
+    Q[1, 3] *= 2
+    Q[2, 3] *= 2
+    roi_u, _ = mvsv.create_dmap_rois((H, W), D)
+    det = mvsv.MeanDisparityDetection()
+    det.init((roi_u[3] - roi_u[1], roi_u[2] - roi_u[0]), Q, 0.1, 1.5)
+    uniq = [mvsv.synth_pair(0x5EED0000 + i, W, H, 0, D) for i in range(8)]
+
+    st = mvsv.DisparityStream(m, W, H, depth=a.depth, grid_roi=roi_u)
+    found = 0
+
+    def consume():
+        nonlocal found
+        d, means = st.pop()
+        det.build(d, 0, det.MEAN_VALUE, means=means)
+        det.detectObstacles(write_pcl=False)
+        found += len(det.getFoundObstacles())
+
+    for i in range(a.depth):  # warm-up
+        st.push(*uniq[i % 8])
+    while st.pending():
+        consume()
+    t0 = time.perf_counter()
+    for i in range(a.frames):
+        if st.pending() == a.depth:
+            consume()
+        st.push(*uniq[i % 8])
+    while st.pending():
+        consume()
+    wall = time.perf_counter() - t0
+    st.close()
+
+    # device-resident rate of the same matcher (8-frame batch already in HBM)
+    dev = torch.device("cuda", 0)
+    Lt = torch.from_numpy(np.stack([u[0] for u in uniq])).to(dev)
+    Rt = torch.from_numpy(np.stack([u[1] for u in uniq])).to(dev)
+    out = torch.empty((8, H, W), dtype=torch.int16, device=dev)
+    for _ in range(2):
+        m.compute(Lt, Rt, out)
+    torch.cuda.synchronize()
+    steps = 10
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        m.compute(Lt, Rt, out)
+        mvsv.mean_disparity_grid(out[:, roi_u[1]:roi_u[3], roi_u[0]:roi_u[2]])
+    torch.cuda.synchronize()
+    dwall = time.perf_counter() - t1
+    print(json.dumps({
+        "workload": f"config5_stream_{W}x{H}_d{D}_mode_sgbm",
+        "frames": a.frames, "depth": a.depth,
+        "stream_fps": round(a.frames / wall, 2),
+        "stream_mpix_s": round(a.frames * W * H / wall / 1e6, 2),
+        "stream_ms_per_frame": round(wall / a.frames * 1e3, 3),
+        "device_resident_mpix_s": round(8 * steps * W * H / dwall / 1e6, 2),
+        "device_resident_ms_per_frame": round(dwall / (8 * steps) * 1e3, 3),
+        "obstacle_tiles_found": found,
+        "note": "stream = host frames in, int16 map + 81 means out (PCIe incl.); "
+                "post-pass = MeanDisparityDetection build(MEAN_VALUE) + detectObstacles",
+    }))
+
+
+if __name__ == "__main__":
+    main()
