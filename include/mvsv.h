@@ -28,6 +28,12 @@
  *                                     trgt/mean_test.cpp:61-70,258-318 (condvar
  *                                     hand-off, Disparity::sgbm, build(MEAN_VALUE))
  *                                     as a double-buffered device pipeline
+ *   mvsv_remap_device / mvsv_rectify  cv::remap(INTER_LINEAR) + ROI crop of
+ *                                     Stereosystem::getRectifiedImagepair
+ *                                     src/Stereosystem.cpp:243-262
+ *   mvsv_init_undistort_rectify_map   cv::initUndistortRectifyMap (CV_32FC1) as
+ *                                     called by Stereosystem::initRectification
+ *                                     src/Stereosystem.cpp:193-237
  *   mvsv_reproject_device             Utility::calcCoordinate src/utility.cpp:176-198,
  *                                     per pixel (the loop of Utility::dmap2pcl :242-262)
  *   mvsv_calc_coordinate / _distance  Utility::calcCoordinate / calcDistance
@@ -216,6 +222,36 @@ MVSV_API int mvsv_stream_push(mvsv_stream* s, const uint8_t* left, size_t left_s
 MVSV_API int mvsv_stream_pop(mvsv_stream* s, int16_t* out, size_t out_stride, float* means);
 MVSV_API int mvsv_stream_pending(const mvsv_stream* s);
 MVSV_API void mvsv_stream_destroy(mvsv_stream* s);
+
+/* ---- before the path: rectification ---------------------------
+ * cv::remap(src, dst, map_x, map_y, INTER_LINEAR) with BORDER_CONSTANT 0 for CV_8UC1
+ * images and CV_32FC1 maps, in OpenCV 3.4's fixed-point arithmetic (INTER_BITS 5,
+ * 15-bit weights): bit-exact for given maps.  n frames (device pointers) share one
+ * map pair (dst_width x dst_height floats each, map_stride floats per row). */
+MVSV_API int mvsv_remap_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t src_stride,
+                               size_t src_frame_stride, int src_width, int src_height,
+                               const float* map_x, const float* map_y, size_t map_stride,
+                               uint8_t* dst, size_t dst_stride, size_t dst_frame_stride,
+                               int dst_width, int dst_height);
+
+/* Stereosystem::getRectifiedImagepair on host buffers: remap both images of a
+ * W x H pair with their map pairs (maps: left x, left y, right x, right y, host,
+ * W x H floats each), then crop to roi (mDisplayROI) into out_left / out_right
+ * ((roi.x1 - roi.x0) x (roi.y1 - roi.y0) bytes). */
+MVSV_API int mvsv_rectify_pair(mvsv_ctx* ctx, const uint8_t* left, size_t left_stride,
+                               const uint8_t* right, size_t right_stride, int width, int height,
+                               const float* const* maps, const mvsv_rect* roi, uint8_t* out_left,
+                               size_t out_left_stride, uint8_t* out_right, size_t out_right_stride);
+
+/* cv::initUndistortRectifyMap(K, dist, R, P, size, CV_32FC1): K 3x3, dist =
+ * (k1, k2, p1, p2[, k3[, k4, k5, k6]]) with ndist in {0, 4, 5, 8}, R 3x3, P 3x3 or
+ * the left 3x3 of a 3x4 projection (row-major doubles).  Double-precision
+ * restatement (inverse of P*R by adjugate; OpenCV uses SVD, so maps may differ
+ * in the last float bit); host only. */
+MVSV_API int mvsv_init_undistort_rectify_map(const double* K, const double* dist, int ndist,
+                                             const double* R, const double* P, int width,
+                                             int height, float* map_x, float* map_y,
+                                             size_t map_stride);
 
 /* ---- after the path: reprojection and point-cloud output ----
  * Q is the 4x4 CV_32F reprojection matrix of stereoRectify, 16 floats row-major

@@ -11,6 +11,7 @@ from ._lib import (MODE_HH, MODE_SGBM, PREFILTER_NORMALIZED_RESPONSE, PREFILTER_
 from .disparity import (Disparity, StereoBM, StereoSGBM, Stereopair, mean_disparity_grid,
                         sgbmParameters, synth_pair)
 from .detection import DisparityStream, MeanDisparityDetection, Subimage, create_dmap_rois
+from .rectify import init_undistort_rectify_map, rectify_pair, remap
 from .utility import Utility, dMapValues, ply, reproject
 
 __all__ = [
@@ -18,6 +19,6 @@ __all__ = [
     "synth_pair", "mean_disparity_grid", "MODE_SGBM", "MODE_HH", "PREFILTER_XSOBEL",
     "PREFILTER_NORMALIZED_RESPONSE", "VARIANT_FIRSTCOL_FIX", "VARIANT_WTA_MIN_D",
     "DisparityStream", "MeanDisparityDetection", "Subimage", "create_dmap_rois", "Utility",
-    "dMapValues", "ply", "reproject",
+    "dMapValues", "ply", "reproject", "init_undistort_rectify_map", "rectify_pair", "remap",
 ]
 __version__ = "1.0.0"

@@ -128,6 +128,9 @@ def _declare(lib, strict=True):
         "mvsv_stream_pop": ([P, P, Z, P], I),
         "mvsv_stream_pending": ([P], I),
         "mvsv_stream_destroy": ([P], None),
+        "mvsv_remap_device": ([P, I, P, Z, Z, I, I, P, P, Z, P, Z, Z, I, I], I),
+        "mvsv_rectify_pair": ([P, P, Z, P, Z, I, I, P, P, P, Z, P, Z], I),
+        "mvsv_init_undistort_rectify_map": ([P, P, I, P, P, I, I, P, P, Z], I),
         "mvsv_reproject_device": ([P, I, P, Z, Z, I, I, P, P, Z, Z], I),
         "mvsv_calc_coordinate": ([ctypes.c_float] * 3 + [P, P], None),
         "mvsv_calc_distance": ([ctypes.c_float] * 3 + [P], ctypes.c_float),

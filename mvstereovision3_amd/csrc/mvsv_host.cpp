@@ -795,3 +795,114 @@ int mvsv_dmap2pcl(mvsv_ctx* ctx, const char* path, const int16_t* dmap, size_t s
     if (rc) return set_error(ctx, rc, "dmap2pcl: map has no positive disparity");
     return MVSV_OK;
 }
+
+// ---- rectification ------------------------------------------
+
+int mvsv_remap_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_t sfs, int sw,
+                      int sh, const float* mx, const float* my, size_t ms, uint8_t* dst, size_t ds,
+                      size_t dfs, int dw, int dh)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    if (n <= 0 || !src || !mx || !my || !dst || sw <= 0 || sh <= 0 || dw <= 0 || dh <= 0 ||
+        ss < (size_t)sw || ds < (size_t)dw || ms < (size_t)dw)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "bad remap arguments");
+    (void)hipSetDevice(ctx->device);
+    return remap_device(ctx, n, src, ss, sfs, sw, sh, mx, my, ms, dst, ds, dfs, dw, dh);
+}
+
+// [Stereosystem::getRectifiedImagepair] src/Stereosystem.cpp:243-262
+int mvsv_rectify_pair(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* R, size_t rs,
+                      int W, int H, const float* const* maps, const mvsv_rect* roi, uint8_t* oL,
+                      size_t ols, uint8_t* oR, size_t ors)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    if (!L || !R || !maps || !roi || !oL || !oR || W <= 0 || H <= 0 || ls < (size_t)W ||
+        rs < (size_t)W || roi->x0 < 0 || roi->y0 < 0 || roi->x1 > W || roi->y1 > H ||
+        roi->x1 <= roi->x0 || roi->y1 <= roi->y0 || ols < (size_t)(roi->x1 - roi->x0) ||
+        ors < (size_t)(roi->x1 - roi->x0))
+        return set_error(ctx, MVSV_E_INVALID_ARG, "bad rectification arguments");
+    for (int i = 0; i < 4; i++)
+        if (!maps[i]) return set_error(ctx, MVSV_E_INVALID_ARG, "null map");
+    (void)hipSetDevice(ctx->device);
+    const size_t px = (size_t)W * H;
+    int rc;
+    if ((rc = ensure(ctx, ctx->h_left, 2 * px, "rectify staging")) ||
+        (rc = ensure(ctx, ctx->h_right, 2 * px, "rectify staging")) ||
+        (rc = ensure(ctx, ctx->h_out, 4 * px * sizeof(float), "rectify maps")))
+        return rc;
+    uint8_t* dsrc = (uint8_t*)ctx->h_left.ptr;   // [2][H][W] inputs
+    uint8_t* ddst = (uint8_t*)ctx->h_right.ptr;  // [2][H][W] outputs
+    float* dmap = (float*)ctx->h_out.ptr;         // [4][H][W]
+    hipStream_t s = ctx->stream;
+    const uint8_t* ins[2] = {L, R};
+    const size_t istr[2] = {ls, rs};
+    for (int i = 0; i < 2; i++)
+        if ((rc = check_hip(ctx, hipMemcpy2DAsync(dsrc + i * px, W, ins[i], istr[i], W, H,
+                                                  hipMemcpyHostToDevice, s), "H2D image")))
+            return rc;
+    for (int i = 0; i < 4; i++)
+        if ((rc = check_hip(ctx, hipMemcpyAsync(dmap + i * px, maps[i], px * sizeof(float),
+                                                hipMemcpyHostToDevice, s), "H2D map")))
+            return rc;
+    for (int i = 0; i < 2; i++)
+        if ((rc = remap_device(ctx, 1, dsrc + i * px, W, px, W, H, dmap + (2 * i) * px,
+                               dmap + (2 * i + 1) * px, W, ddst + i * px, W, px, W, H)))
+            return rc;
+    const int cw = roi->x1 - roi->x0, ch = roi->y1 - roi->y0;
+    uint8_t* outs[2] = {oL, oR};
+    const size_t ostr[2] = {ols, ors};
+    for (int i = 0; i < 2; i++)
+        if ((rc = check_hip(ctx, hipMemcpy2DAsync(outs[i], ostr[i],
+                                                  ddst + i * px + (size_t)roi->y0 * W + roi->x0, W, cw,
+                                                  ch, hipMemcpyDeviceToHost, s), "D2H image")))
+            return rc;
+    return check_hip(ctx, hipStreamSynchronize(s), "hipStreamSynchronize");
+}
+
+// [cv::initUndistortRectifyMap] (OpenCV 3.4 undistort.cpp), CV_32FC1 output
+int mvsv_init_undistort_rectify_map(const double* K, const double* dist, int ndist,
+                                    const double* Rm, const double* P, int W, int H, float* mx,
+                                    float* my, size_t ms)
+{
+    if (!K || !P || !mx || !my || W <= 0 || H <= 0 || ms < (size_t)W ||
+        !(ndist == 0 || ndist == 4 || ndist == 5 || ndist == 8) || (ndist && !dist))
+        return MVSV_E_INVALID_ARG;
+    const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    const double* R = Rm ? Rm : I3;
+    // A = P[:, :3] * R; iR = A^-1
+    double A[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double acc = 0;
+            for (int k = 0; k < 3; k++) acc += P[i * 3 + k] * R[k * 3 + j];
+            A[i * 3 + j] = acc;
+        }
+    const double det = A[0] * (A[4] * A[8] - A[5] * A[7]) - A[1] * (A[3] * A[8] - A[5] * A[6]) +
+                       A[2] * (A[3] * A[7] - A[4] * A[6]);
+    if (det == 0) return MVSV_E_INVALID_ARG;
+    double ir[9] = {(A[4] * A[8] - A[5] * A[7]) / det, (A[2] * A[7] - A[1] * A[8]) / det,
+                    (A[1] * A[5] - A[2] * A[4]) / det, (A[5] * A[6] - A[3] * A[8]) / det,
+                    (A[0] * A[8] - A[2] * A[6]) / det, (A[2] * A[3] - A[0] * A[5]) / det,
+                    (A[3] * A[7] - A[4] * A[6]) / det, (A[1] * A[6] - A[0] * A[7]) / det,
+                    (A[0] * A[4] - A[1] * A[3]) / det};
+    double k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < ndist; i++) k[i] = dist[i];
+    const double k1 = k[0], k2 = k[1], p1 = k[2], p2 = k[3], k3 = k[4], k4 = k[5], k5 = k[6], k6 = k[7];
+    const double u0 = K[2], v0 = K[5], fx = K[0], fy = K[4];
+    for (int i = 0; i < H; i++) {
+        float* m1 = mx + (size_t)i * ms;
+        float* m2 = my + (size_t)i * ms;
+        double _x = i * ir[1] + ir[2], _y = i * ir[4] + ir[5], _w = i * ir[7] + ir[8];
+        for (int j = 0; j < W; j++, _x += ir[0], _y += ir[3], _w += ir[6]) {
+            const double w = 1. / _w, x = _x * w, y = _y * w;
+            const double x2 = x * x, y2 = y * y;
+            const double r2 = x2 + y2, _2xy = 2 * x * y;
+            const double kr = (1 + ((k3 * r2 + k2) * r2 + k1) * r2) / (1 + ((k6 * r2 + k5) * r2 + k4) * r2);
+            const double u = fx * (x * kr + p1 * _2xy + p2 * (r2 + 2 * x2)) + u0;
+            const double v = fy * (y * kr + p1 * (r2 + 2 * y2) + p2 * _2xy) + v0;
+            m1[j] = (float)u;
+            m2[j] = (float)v;
+        }
+    }
+    return MVSV_OK;
+}

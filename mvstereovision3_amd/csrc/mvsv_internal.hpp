@@ -123,6 +123,9 @@ int median3x3_device(mvsv_ctx* ctx, int n, const int16_t* src, size_t ss, size_t
                      int16_t* dst, size_t ds, size_t dfs, int W, int H);
 int speckle_device(mvsv_ctx* ctx, int n, int16_t* img, size_t st, size_t fs, int W, int H,
                    int new_val, int max_size, int max_diff);
+int remap_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_t sfs, int sw, int sh,
+                 const float* mx, const float* my, size_t ms, uint8_t* dst, size_t ds, size_t dfs,
+                 int dw, int dh);
 int reproject_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_t fs, int W, int H,
                      const float* Q, float* out, size_t os, size_t ofs);
 int mean_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_t fs, int W,

@@ -339,6 +339,47 @@ __global__ __launch_bounds__(256) void mean_grid_kernel(const int16_t* __restric
     }
 }
 
+// ---- cv::remap(INTER_LINEAR, BORDER_CONSTANT 0), CV_8UC1, CV_32FC1 maps ----------
+// The rectification step of Stereosystem::getRectifiedImagepair
+// (src/Stereosystem.cpp:243-262).  [OpenCV 3.4 RemapInvoker + remapBilinear]:
+// X = cvRound(mapx * 32), Y = cvRound(mapy * 32) (round half to even);
+// (sx, sy) = (X >> 5, Y >> 5) saturated to short, (ax, ay) = the low 5 bits;
+// weights (32-ay)(32-ax)*32, (32-ay)ax*32, ay(32-ax)*32, ay*ax*32 (sum 2^15,
+// exact for bilinear); out = (sum + 2^14) >> 15.  A 2x2 footprint entirely
+// outside the source gives 0; partially outside, the outside taps read 0.
+__device__ __forceinline__ int remap_tap(const uint8_t* s, size_t ss, int W, int H, int x, int y)
+{
+    return (x >= 0 && x < W && y >= 0 && y < H) ? (int)s[(size_t)y * ss + x] : 0;
+}
+
+__global__ __launch_bounds__(256) void remap_linear_kernel(
+    const uint8_t* __restrict__ src, size_t ss, size_t sfs, int sw, int sh,
+    const float* __restrict__ mx, const float* __restrict__ my, size_t ms,
+    uint8_t* __restrict__ dst, size_t ds, size_t dfs, int dw, int dh)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.z;
+    if (x >= dw || y >= dh) return;
+    const int X = __float2int_rn(mx[(size_t)y * ms + x] * 32.0f);
+    const int Y = __float2int_rn(my[(size_t)y * ms + x] * 32.0f);
+    const int sx = clampi(X >> 5, -32768, 32767), sy = clampi(Y >> 5, -32768, 32767);
+    const int ax = X & 31, ay = Y & 31;
+    const uint8_t* s = src + f * sfs;
+    int v;
+    if (sx >= sw || sx + 1 < 0 || sy >= sh || sy + 1 < 0) {
+        v = 0;
+    } else {
+        const int w00 = (32 - ay) * (32 - ax) * 32, w01 = (32 - ay) * ax * 32;
+        const int w10 = ay * (32 - ax) * 32, w11 = ay * ax * 32;
+        const int acc = remap_tap(s, ss, sw, sh, sx, sy) * w00 + remap_tap(s, ss, sw, sh, sx + 1, sy) * w01 +
+                        remap_tap(s, ss, sw, sh, sx, sy + 1) * w10 +
+                        remap_tap(s, ss, sw, sh, sx + 1, sy + 1) * w11;
+        v = clampi((acc + (1 << 14)) >> 15, 0, 255);
+    }
+    dst[f * dfs + (size_t)y * ds + x] = (uint8_t)v;
+}
+
 // ---- Utility::calcCoordinate per pixel (src/utility.cpp:176-198) -------------
 // (X, Y, Z, W) = Q * (x, y, v / 16, 1) with OpenCV's float GEMM (products and
 // sums in double, one rounding to float per element), then Mat /= W as
@@ -416,6 +457,16 @@ int mean_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_
     hipLaunchKernelGGL(mean_grid_kernel, dim3(81, n), dim3(256), 0, ctx->stream, dmap, st, fs, W,
                        H, means);
     return check_hip(ctx, hipGetLastError(), "mean disparity grid");
+}
+
+int remap_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_t sfs, int sw, int sh,
+                 const float* mx, const float* my, size_t ms, uint8_t* dst, size_t ds, size_t dfs,
+                 int dw, int dh)
+{
+    dim3 grid((dw + 63) / 64, (dh + 3) / 4, n);
+    hipLaunchKernelGGL(remap_linear_kernel, grid, dim3(256), 0, ctx->stream, src, ss, sfs, sw, sh,
+                       mx, my, ms, dst, ds, dfs, dw, dh);
+    return check_hip(ctx, hipGetLastError(), "remap");
 }
 
 int reproject_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_t fs, int W, int H,

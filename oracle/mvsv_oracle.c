@@ -857,3 +857,48 @@ void orc_reproject(const int16_t* dmap, ptrdiff_t st, int W, int H, const float*
             o[3] = v > 0 ? 1.0f : 0.0f;
         }
 }
+
+/* [OpenCV 3.4 imgproc/src/imgwarp.cpp] RemapInvoker (CV_32FC1 maps -> fixed point:
+ * X = saturate_cast<int>(mapx * INTER_TAB_SIZE), XY = X >> INTER_BITS, A = low bits)
+ * and remapBilinear<FixedPtCast<int, uchar, 15>> with initInterTab2D's integer
+ * bilinear table (exact for INTER_LINEAR: weights * 32768 are integers). */
+static int orc_round_f(float v)
+{
+    if (v != v) return INT_MIN;
+    if (v >= 2147483648.0f) return INT_MAX;
+    if (v < -2147483648.0f) return INT_MIN;
+    return (int)lrintf(v); /* cvRound: round half to even */
+}
+
+void orc_remap_linear(const uint8_t* src, ptrdiff_t ss, int sw, int sh, const float* mapx,
+                      const float* mapy, uint8_t* dst, int dw, int dh)
+{
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++) {
+            int X = orc_round_f(mapx[(size_t)y * dw + x] * 32);
+            int Y = orc_round_f(mapy[(size_t)y * dw + x] * 32);
+            int sx = X >> 5, sy = Y >> 5;
+            if (sx < -32768) sx = -32768;
+            if (sx > 32767) sx = 32767;
+            if (sy < -32768) sy = -32768;
+            if (sy > 32767) sy = 32767;
+            int ax = X & 31, ay = Y & 31;
+            int v;
+            if (sx >= sw || sx + 1 < 0 || sy >= sh || sy + 1 < 0) {
+                v = 0;
+            } else {
+                int w[4] = {(32 - ay) * (32 - ax) * 32, (32 - ay) * ax * 32, ay * (32 - ax) * 32,
+                            ay * ax * 32};
+                int xs[4] = {sx, sx + 1, sx, sx + 1}, ys[4] = {sy, sy, sy + 1, sy + 1};
+                int acc = 0;
+                for (int t = 0; t < 4; t++) {
+                    int inside = xs[t] >= 0 && xs[t] < sw && ys[t] >= 0 && ys[t] < sh;
+                    acc += (inside ? src[(ptrdiff_t)ys[t] * ss + xs[t]] : 0) * w[t];
+                }
+                v = (acc + (1 << 14)) >> 15;
+                if (v < 0) v = 0;
+                if (v > 255) v = 255;
+            }
+            dst[(size_t)y * dw + x] = (uint8_t)v;
+        }
+}

@@ -94,6 +94,12 @@ int orc_filter_speckles_s16(int16_t* img, ptrdiff_t stride, int W, int H,
 /* MeanDisparityDetection::build(MEAN_VALUE) post-pass: 81 tile means over a
  * CV_16S map (src/MeanDisparityDetection.cpp:159-206, Utility::
  * calcMeanDisparity src/utility.cpp:265-285). means[81] row-major tiles. */
+/* cv::remap(src, dst, mapx, mapy, INTER_LINEAR, BORDER_CONSTANT, 0), CV_8UC1 with
+ * CV_32FC1 maps (OpenCV 3.4 RemapInvoker map conversion + remapBilinear).
+ * dst is dw x dh (stride dw), maps dw x dh (stride dw). */
+void orc_remap_linear(const uint8_t* src, ptrdiff_t sstride, int sw, int sh, const float* mapx,
+                      const float* mapy, uint8_t* dst, int dw, int dh);
+
 /* Utility::calcCoordinate (src/utility.cpp:176-198) for every pixel:
  * out[y][x] = (X, Y, Z, v > 0), Q 4x4 CV_32F row-major.  OpenCV float Mat
  * product (double accumulation over k = 0..3, one rounding), then Mat /= W

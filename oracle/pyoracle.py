@@ -63,6 +63,7 @@ def lib():
         _lib.orc_filter_speckles_s16.restype = I
         _lib.orc_mean_disparity_grid.argtypes = [P, S, I, I, P]
         _lib.orc_reproject.argtypes = [P, S, I, I, P, P]
+        _lib.orc_remap_linear.argtypes = [P, S, I, I, P, P, P, I, I]
     return _lib
 
 
@@ -160,4 +161,16 @@ def reproject(dmap: np.ndarray, Q) -> np.ndarray:
     q = np.ascontiguousarray(np.asarray(Q, np.float32).reshape(16))
     out = np.empty((H, W, 4), np.float32)
     lib().orc_reproject(_ptr(d), W, W, H, _ptr(q), _ptr(out))
+    return out
+
+
+def remap_linear(src: np.ndarray, mapx: np.ndarray, mapy: np.ndarray) -> np.ndarray:
+    """cv::remap(INTER_LINEAR, BORDER_CONSTANT 0) of a uint8 image with float32 maps."""
+    s = np.ascontiguousarray(src, np.uint8)
+    mx = np.ascontiguousarray(mapx, np.float32)
+    my = np.ascontiguousarray(mapy, np.float32)
+    dh, dw = mx.shape
+    out = np.empty((dh, dw), np.uint8)
+    lib().orc_remap_linear(_ptr(s), s.shape[1], s.shape[1], s.shape[0], _ptr(mx), _ptr(my),
+                           _ptr(out), dw, dh)
     return out

@@ -401,3 +401,34 @@ def test_disparity_stream_matches_direct_compute(gpu, mvsv, oracle):
         assert np.array_equal(d, want), f"frame {i}: " + report(d, want)
         x0, y0, x1, y1 = roi_u
         assert np.array_equal(means, oracle.mean_disparity_grid(np.ascontiguousarray(want[y0:y1, x0:x1])))
+
+
+# ----------------------------------------------------------- f2: remap -----
+def test_remap_matches_oracle(gpu, mvsv, oracle):
+    import torch
+    rng = np.random.default_rng(21)
+    H, W = 120, 200
+    img = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    K = np.array([[150.0, 0, 100], [0, 150.0, 60], [0, 0, 1]])
+    R = np.array([[0.9998, -0.01, 0.0174], [0.0102, 0.9999, -0.005], [-0.0174, 0.0052, 0.9998]])
+    mx, my = mvsv.init_undistort_rectify_map(K, [-0.25, 0.07, 0.001, -0.0015, 0.0], R, K, (W, H))
+    mx[0, :4] = [-3.0, 199.5, 200.2, np.float32(1 / 64)]  # border cases + a half-way rounding
+    got = mvsv.remap(torch.from_numpy(img).cuda(), torch.from_numpy(mx).cuda(),
+                     torch.from_numpy(my).cuda()).cpu().numpy()
+    assert np.array_equal(got, oracle.remap_linear(img, mx, my))
+
+
+def test_rectify_pair_then_sgbm(gpu, mvsv, oracle):
+    """Stereosystem::getRectifiedImagepair + Disparity::sgbm on the cropped pair."""
+    L, R = mvsv.synth_pair(SEED0 + 60, 240, 100, 0, 32)
+    yy, xx = np.mgrid[0:100, 0:240].astype(np.float32)
+    maps = (xx + 0.25, yy, xx - 0.25, yy + 0.5)
+    roi = (4, 2, 236, 98)
+    rl, rr = mvsv.rectify_pair(L, R, maps, roi)
+    x0, y0, x1, y1 = roi
+    assert np.array_equal(rl, oracle.remap_linear(L, maps[0], maps[1])[y0:y1, x0:x1])
+    assert np.array_equal(rr, oracle.remap_linear(R, maps[2], maps[3])[y0:y1, x0:x1])
+    d = mvsv.StereoSGBM.create(0, 32, 5).compute(rl, rr)
+    p = dict(mvsv.StereoSGBM.create(0, 32, 5).params())
+    p.pop("variant")
+    assert np.array_equal(d, oracle.sgbm(rl, rr, p))
