@@ -1381,20 +1381,95 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
 // order-independent atomicMin on keys (minS << 16 | 0xFFFF - x): smallest cost,
 // then the largest x -- exactly OpenCV's descending scan with a strict '>'.
 // ---------------------------------------------------------------------------
-constexpr int kFinal16PF = 4;
+
+// Raw accumulator words of one lane (2*NP disparities): the NACC planes are
+// summed in storage format -- u8 bytes never carry because the total over all
+// directions is <= ndir*P2 <= 255 (acc_is_u8) -- and unpacked to u16 pairs once.
+template <int NP, typename AccT>
+struct AccRaw;
+template <int NP>
+struct AccRaw<NP, uint8_t> {
+    static constexpr int NW = NP >= 2 ? NP / 2 : 1;
+    static __device__ __forceinline__ void load(const uint8_t* p, uint32_t (&w)[NW])
+    {
+        if constexpr (NP == 1) {
+            w[0] = *(const uint16_t*)p;
+        } else if constexpr (NP == 2) {
+            w[0] = *(const uint32_t*)p;
+        } else if constexpr (NP == 4) {
+            const uint2 t = *(const uint2*)p;
+            w[0] = t.x;
+            w[1] = t.y;
+        } else {
+            const uint4 t = *(const uint4*)p;
+            w[0] = t.x;
+            w[1] = t.y;
+            w[2] = t.z;
+            w[3] = t.w;
+        }
+    }
+    static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) { return a + b; }
+    static __device__ __forceinline__ void unpack(const uint32_t (&w)[NW], uint32_t (&v)[NP])
+    {
+#pragma unroll
+        for (int p = 0; p < NP; p++) v[p] = u8x2_to_u16x2(w[p >> 1], p & 1);
+    }
+};
+template <int NP>
+struct AccRaw<NP, uint16_t> {
+    static constexpr int NW = NP;
+    static __device__ __forceinline__ void load(const uint16_t* p, uint32_t (&w)[NW])
+    {
+        AccVec<NP, uint16_t>::load(p, w);
+    }
+    static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b)
+    {
+        return AccVec<NP, uint16_t>::add(a, b);
+    }
+    static __device__ __forceinline__ void unpack(const uint32_t (&w)[NW], uint32_t (&v)[NP])
+    {
+#pragma unroll
+        for (int p = 0; p < NP; p++) v[p] = w[p];
+    }
+};
+
+// Steps of C / accumulator prefetch: as deep as ~160 VGPRs of buffers allow
+// (a power of two dividing the 16-step flush period).  The kernel is bound by
+// load latency at ~2 waves per SIMD, so depth is what buys bandwidth.
+template <int NP, int NACC, typename AccT, bool UQ>
+constexpr int final16_pf()
+{
+    constexpr int words = NP + NACC * AccRaw<NP, AccT>::NW;  // VGPRs per step
+    constexpr int budget = UQ ? 96 : 160;
+    return budget / words >= 16 ? 16 : (budget / words >= 8 ? 8 : 4);
+}
+
+// a * b + c per u16 half, saturated at 0xffff (VOP3P clamp)
+__device__ __forceinline__ uint32_t pk_mad_u16_clamp(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, %2, %3 clamp" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 
 // NACC accumulator planes (A + i * plane) hold the summed deltas of disjoint
 // direction groups written by concurrent passes; their sum is the S input.
-template <int NP, int NACC, typename AccT>
-__global__ __launch_bounds__(64) void sgbm_final16_kernel(const int16_t* __restrict__ C,
+// UQ: uniquenessRatio > 0.
+template <int NP, int NACC, typename AccT, bool UQ>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 : 2))) void sgbm_final16_kernel(const int16_t* __restrict__ C,
                                                          const AccT* __restrict__ A, size_t plane,
                                                          int H, int W, SgbmEff e,
                                                          int16_t* __restrict__ raw,
-                                                         uint32_t* __restrict__ keys)
+                                                         uint32_t* __restrict__ keys,
+                                                         int16_t* __restrict__ dummy)
 {
-    using AV = AccVec<NP, AccT>;
-    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    constexpr int PF = kFinal16PF;
+    using AR = AccRaw<NP, AccT>;
+    constexpr int NW = AR::NW;
+    constexpr int PF = final16_pf<NP, NACC, AccT, UQ>();
+    constexpr int DR = 32 * NP;  // disparities of a row (D)
+    // S of the current step, one D-vector per row: S[best -+ 1] come back
+    // through LDS instead of lane shuffles.
+    __shared__ __attribute__((aligned(16))) uint16_t srow[4 * DR];
     const int lane = threadIdx.x;
     const int row = lane >> 4, rl = lane & 15;
     const int yr = blockIdx.x * 4 + row;
@@ -1419,136 +1494,140 @@ __global__ __launch_bounds__(64) void sgbm_final16_kernel(const int16_t* __restr
     const size_t off = f * frame + ((size_t)y * W1 + (W1 - 1)) * D + d0;
     const int16_t* cp = C + off;
     const AccT* sp = A + off;
+    uint16_t* ms = srow + row * DR;
     uint32_t lp[NP];
 #pragma unroll
     for (int p = 0; p < NP; p++) lp[p] = 0u;
     const uint32_t p1x2 = (uint32_t)(e.P1 & 0xffff) * 0x10001u;
     const uint32_t p2x2 = (uint32_t)(e.P2 & 0xffff) * 0x10001u;
-    const bool eight = e.fullDP != 0;
+    // S = min(ndir*(C - P2) + sum of deltas, MAX_COST) = min((ndir-1)*cb + L + acc, MAX_COST)
+    // with cb = C - P2, L = cb + delta of the R->L direction computed here
+    const uint32_t ndm1 = (uint32_t)(e.fullDP ? 7 : 4) * 0x10001u;
     const int uq = e.uniq;
-    const int rowbase = lane & ~15;
+    // tie order of the WTA key: d, or OpenCV's SIMD lane order for MODE_SGBM
+    uint32_t subk[2 * NP];
+#pragma unroll
+    for (int i = 0; i < 2 * NP; i++) {
+        const int d = d0 + i;
+        subk[i] = lane_rule ? (uint32_t)(((d & 7) << 12) | (d >> 3)) : (uint32_t)d;
+    }
+    uint32_t dpair[NP];  // (d, d + 1) of each packed pair
+#pragma unroll
+    for (int p = 0; p < NP; p++) dpair[p] = (uint32_t)(d0 + 2 * p) | ((uint32_t)(d0 + 2 * p + 1) << 16);
     int minp = 0;
 
     Vec<NP> cb[PF];
-    uint32_t sb[PF][NP];
-    auto acc_load = [&](const AccT* q, uint32_t (&v)[NP]) {
-        AV::load(q, v);
+    uint32_t ab[PF][NACC][NW];
+    auto prefetch = [&](int j, ptrdiff_t t) {
+        cb[j].load(cp - t * D);
 #pragma unroll
-        for (int i = 1; i < NACC; i++) {
-            uint32_t u[NP];
-            AV::load(q + i * plane, u);
-#pragma unroll
-            for (int p = 0; p < NP; p++) v[p] = AV::add(v[p], u[p]);
-        }
+        for (int i = 0; i < NACC; i++) AR::load(sp - t * D + i * plane, ab[j][i]);
     };
 #pragma unroll
-    for (int j = 0; j < PF; j++) {
-        const ptrdiff_t t = min(j, W1 - 1);
-        cb[j].load(cp - t * D);
-        acc_load(sp - t * D, sb[j]);
-    }
-    // Per step the row's 16 lanes agree on K = (minS << 16 | lane-rule sub),
-    // S[best-1], S[best+1] and the uniqueness verdict; lane (s & 15) keeps them,
-    // and every 16 steps the 16 lanes finish 16 columns at once (sub-pixel
-    // division, raw store, right-view atomicMin) -- the per-step path stays
-    // branch-free so consecutive steps overlap.
-    uint32_t kK = 0xffffffffu, kS = 0;  // kept: K, (Sp << 16 | Sm & 0xffff)
-    int kRej = 0;
+    for (int j = 0; j < PF; j++) prefetch(j, min(j, W1 - 1));
+    // Per step the row's 16 lanes agree on K = (minS << 16 | tie-order sub),
+    // S[best-1], S[best+1] and the uniqueness verdict; they park that record in
+    // LDS slot (s & 15) of the row, and every 16 steps lane rl picks up record
+    // rl and the 16 lanes finish 16 columns at once (sub-pixel division, raw
+    // store, right-view atomicMin) -- the per-step path stays branch-free so
+    // consecutive steps overlap.
+    __shared__ uint2 srec[4 * 16];
+    uint2* recs = srec + row * 16;
     auto body = [&](int s, int j) {
         const int dl = (int16_t)(minp + e.P2);
         const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
-        uint32_t c[NP], ln[NP], st[NP];
+        uint32_t c[NP], ln[NP], st[NP], acc[NP], w[NW];
 #pragma unroll
         for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
         sgm_step_row<NP>(lp, delta2, p1x2, c, ln);
         minp = row_min_i32(lane_min_row<NP>(ln));
-        int key = 0x7fffffff;
+#pragma unroll
+        for (int k = 0; k < NW; k++) {
+            w[k] = ab[j][0][k];
+#pragma unroll
+            for (int i = 1; i < NACC; i++) w[k] = AR::add(w[k], ab[j][i][k]);
+        }
+        AR::unpack(w, acc);
+        uint32_t key = 0x7fffffffu;
 #pragma unroll
         for (int p = 0; p < NP; p++) {
-            // S = min(ndir*(C - P2) + sum of deltas, MAX_COST), saturating u16
-            u16x2 cbv = __builtin_bit_cast(u16x2, c[p]) - __builtin_bit_cast(u16x2, p2x2);
-            u16x2 x2v = __builtin_elementwise_add_sat(cbv, cbv);
-            u16x2 x4 = __builtin_elementwise_add_sat(x2v, x2v);
-            u16x2 t = eight ? __builtin_elementwise_add_sat(x4, x4)
-                            : __builtin_elementwise_add_sat(x4, cbv);
-            u16x2 acc = __builtin_elementwise_add_sat(
-                __builtin_bit_cast(u16x2, sb[j][p]),
-                __builtin_bit_cast(u16x2, path_delta(ln[p], c[p], p2x2)));
-            u16x2 sv = __builtin_elementwise_min(__builtin_elementwise_add_sat(t, acc),
-                                                 (u16x2){32767, 32767});
-            st[p] = __builtin_bit_cast(uint32_t, sv);
+            const uint32_t cbv = pk_sub_u16(c[p], p2x2);
+            const uint32_t sv = pk_mad_u16_clamp(cbv, ndm1, pk_add_u16(ln[p], acc[p]));
+            st[p] = pk_min_u16(sv, 0x7fff7fffu);
             lp[p] = ln[p];
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                int d = d0 + 2 * p + h;
-                int v = h ? hi16(st[p]) : lo16(st[p]);
-                int sub = lane_rule ? (((d & 7) << 12) | (d >> 3)) : d;
-                key = min(key, (v << 16) | sub);
-            }
+            const uint32_t klo = (st[p] << 16) | subk[2 * p];
+            const uint32_t khi = (st[p] & 0xffff0000u) | subk[2 * p + 1];
+            key = min(key, min(klo, khi));
         }
-        const int K = row_min_i32(key);
+        const int K = row_min_i32((int)key);
         const int minS = K >> 16;
         const int sub = K & 0xffff;
         const int best = lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
+        // S[best -+ 1] (clamped into [0, D)) through the row's LDS vector
+        {
+            Vec<NP> o;
+#pragma unroll
+            for (int p = 0; p < NP; p++) o.v[p] = st[p];
+            o.store((int16_t*)(ms + d0));
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int bm = max(best - 1, 0), bp = min(best + 1, DR - 1);
+        const int Sm = ms[bm], Sp = ms[bp];
         int rej = 0;
-        if (uq != 0) {  // with uq == 0 the test reads S[d] < minS: never true
+        if constexpr (UQ) {
+            // min of S outside [best-1, best+1]: y = best + 1 - d is <= 2
+            // (unsigned) exactly there; those cells are lifted to >= 0xfffd
+            const uint32_t b2 = (uint32_t)(best + 1) * 0x10001u;
+            uint32_t m2 = 0xffffffffu;
 #pragma unroll
             for (int p = 0; p < NP; p++) {
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    int d = d0 + 2 * p + h;
-                    int v = h ? hi16(st[p]) : lo16(st[p]);
-                    rej |= (v * (100 - uq) < minS * 100) && (abs(best - d) > 1);
-                }
+                const uint32_t yv = pk_sub_u16(b2, dpair[p]);
+                const uint32_t lift = pk_sub_u16(pk_min_u16(yv, 0x00030003u), 0x00030003u);
+                m2 = pk_min_u16(m2, pk_max_u16(st[p], lift));
             }
-            rej = row_max_i32(rej);
+            const int m2r = row_min_i32((int)min(m2 & 0xffffu, m2 >> 16));
+            rej = m2r < 0xfffd && m2r * (100 - uq) < minS * 100;
         }
-        // S[best-1], S[best+1] from the owning lanes of the row
-        auto fetch = [&](int d) -> int {
-            d = clampi(d, 0, D - 1);
-            const int owner = d / (2 * NP), el = d - owner * 2 * NP;
-            uint32_t v = st[0];
-#pragma unroll
-            for (int p = 1; p < NP; p++) v = ((el >> 1) == p) ? st[p] : v;
-            uint32_t w = (uint32_t)__shfl((int)v, rowbase + owner, 64);
-            return (el & 1) ? hi16(w) : lo16(w);
-        };
-        const int Sm = fetch(best - 1), Sp = fetch(best + 1);
-        const bool mine = rl == (s & 15);
-        kK = mine ? (uint32_t)K : kK;
-        kS = mine ? (((uint32_t)Sp << 16) | ((uint32_t)Sm & 0xffffu)) : kS;
-        kRej = mine ? rej : kRej;
+        recs[s & 15] = make_uint2((uint32_t)K | ((uint32_t)rej << 31),
+                                  ((uint32_t)Sp << 16) | ((uint32_t)Sm & 0xffffu));
+        __builtin_amdgcn_wave_barrier();
     };
     // lane rl finishes column s0 + rl of the sweep (x = W1 - 1 - s)
+    // Branch-free around memory (so the prefetch loads keep their exact
+    // vmcnt accounting across the flush): a lane without a column stores to
+    // its dummy slot, a rejected column rewrites INVALID, and an atomicMin
+    // that must not count carries the all-ones key (a no-op).
+    int16_t* dslot = dummy + (blockIdx.x & 63) * 64 + lane;
     auto flush = [&](int s0, int cnt) {
         const int s = s0 + rl;
-        if (!exists || rl >= cnt || kRej) return;
+        const bool own = exists && rl < cnt;
+        const uint2 rec = recs[rl];
+        const uint32_t kK = rec.x & 0x7fffffffu, kS = rec.y;
+        const int kRej = (int)(rec.x >> 31);
         const int minS = (int)(kK >> 16);
         const int sub = (int)(kK & 0xffffu);
         int best = lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
         if (minS >= kMaxCost) best = -1;  // no strict minimum below MAX_COST
         const int Sm = (int)(int16_t)(kS & 0xffffu), Sp = (int)(int16_t)(kS >> 16);
         const int x = W1 - 1 - s;
-        int d16;
-        if (0 < best && best < D - 1) {
-            const int den = max(Sm + Sp - 2 * minS, 1);
-            d16 = best * kDispScale + ((Sm - Sp) * kDispScale + den) / (den * 2);
-        } else {
-            d16 = best * kDispScale;
-        }
-        orow[x + minX1] = (int16_t)(d16 + minD * kDispScale);
+        const int den = max(Sm + Sp - 2 * minS, 1);
+        const int frac = ((Sm - Sp) * kDispScale + den) / (den * 2);
+        // arithmetic mask, not a select: the division stays unconditional (no
+        // branch inside the loop body)
+        const int d16 = best * kDispScale + (frac & -(int)(0 < best && best < D - 1));
+        const int16_t v = kRej ? (int16_t)INV : (int16_t)(d16 + minD * kDispScale);
+        *(own ? orow + x + minX1 : dslot) = v;
         const int x2 = x + minX1 - best - minD;
-        if (minS < kMaxCost && x2 >= 0 && x2 < W)
-            atomicMin(krow + x2, ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
+        const bool hit = own && !kRej && minS < kMaxCost && x2 >= 0 && x2 < W;
+        atomicMin(krow + clampi(x2, 0, W - 1),
+                  hit ? (((uint32_t)minS << 16) | (uint32_t)(0xffff - x)) : 0xffffffffu);
     };
     int s = 0;
     for (; s + 16 <= W1; s += 16) {
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             body(s + j, j % PF);
-            const ptrdiff_t t = min(s + j + PF, W1 - 1);
-            cb[j % PF].load(cp - t * D);
-            acc_load(sp - t * D, sb[j % PF]);
+            prefetch(j % PF, min(s + j + PF, W1 - 1));
         }
         flush(s, 16);
     }
@@ -1557,9 +1636,7 @@ __global__ __launch_bounds__(64) void sgbm_final16_kernel(const int16_t* __restr
     for (int j = 0; j < 16; j++) {
         if (j < rem) {
             body(s + j, j % PF);
-            const ptrdiff_t t = min(s + j + PF, W1 - 1);
-            cb[j % PF].load(cp - t * D);
-            acc_load(sp - t * D, sb[j % PF]);
+            prefetch(j % PF, min(s + j + PF, W1 - 1));
         }
     }
     if (rem > 0) flush(s, rem);
@@ -1773,6 +1850,20 @@ __global__ void fill_s16_kernel(int16_t* __restrict__ out, size_t os, size_t ofs
 }
 
 // sheared-strip schedule: enabled, and int32 element offsets cover a frame
+template <int NP, int NACC, typename AccT>
+void launch_final16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv,
+                    const AccT* Av, size_t plane, int16_t* raw)
+{
+    if (e.uniq > 0)
+        hipLaunchKernelGGL((sgbm_final16_kernel<NP, NACC, AccT, true>), dim3((H + 3) / 4, n),
+                           dim3(64), 0, ctx->stream, Cv, Av, plane, H, W, e, raw,
+                           (uint32_t*)ctx->keys.ptr, (int16_t*)ctx->dummy.ptr);
+    else
+        hipLaunchKernelGGL((sgbm_final16_kernel<NP, NACC, AccT, false>), dim3((H + 3) / 4, n),
+                           dim3(64), 0, ctx->stream, Cv, Av, plane, H, W, e, raw,
+                           (uint32_t*)ctx->keys.ptr, (int16_t*)ctx->dummy.ptr);
+}
+
 static bool use_strips(const mvsv_ctx* ctx, const SgbmEff& e, int H)
 {
     return ctx->tri && (size_t)H * e.W1 * e.D < ((size_t)1 << 31);
@@ -1885,11 +1976,9 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
     }
     StageTimer tm(ctx, kStageFinal);
     if (npass == 2)
-        hipLaunchKernelGGL((sgbm_final16_kernel<NP, 3, AccT>), dim3((H + 3) / 4, n), dim3(64), 0, s,
-                           Cv, Av, plane, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
+        launch_final16<NP, 3, AccT>(ctx, n, H, W, e, Cv, Av, plane, raw);
     else
-        hipLaunchKernelGGL((sgbm_final16_kernel<NP, 2, AccT>), dim3((H + 3) / 4, n), dim3(64), 0, s,
-                           Cv, Av, plane, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
+        launch_final16<NP, 2, AccT>(ctx, n, H, W, e, Cv, Av, plane, raw);
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels (sheared strips)");
 }
 
@@ -1921,8 +2010,7 @@ int launch_paths16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t
                                Av, dummy, H, e.W1, e.D, dx, dy, e.P1, e.P2);
     }
     StageTimer tm(ctx, kStageFinal);
-    hipLaunchKernelGGL((sgbm_final16_kernel<NP, 1, AccT>), dim3((H + 3) / 4, n), dim3(64), 0, s, Cv,
-                       Av, plane, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
+    launch_final16<NP, 1, AccT>(ctx, n, H, W, e, Cv, Av, plane, raw);
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels (16-lane)");
 }
 
