@@ -383,7 +383,8 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int SH2 = NR / 2;
-    const int D = e.D, W1 = e.W1, SW2 = e.SW2;
+    constexpr int SW2 = SH2;  // StereoSGBM's window is square (SW = SH = blockSize)
+    const int D = e.D, W1 = e.W1;
     const Cost2Layout lay = cost2_layout(D, SW2, TY);
     const int PP = lay.PP, CL = lay.CL, TX = lay.TX, NX = lay.NX;
     const int f = blockIdx.z;
@@ -396,7 +397,6 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
     const int rtop = e.minX1 + xchi - e.minD;  // right column of reversed item j = 0
     const size_t plane = (size_t)W * H;
     const uint64_t* PL = pre + (size_t)f * 2 * plane;
-    const uint64_t* PR = PL + plane;
     const int tid = threadIdx.x;
     const int cl = tid / PP, p = tid - cl * PP;
     const bool worker = cl < CL;
@@ -407,25 +407,33 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
     const bool linear = x0 - SW2 >= 0 && x0 + TX + SW2 <= W1 && (CL & 1) == 0;
 
     // staging: item i < nL -> left column ilo + i; else right pair j = i - nL
-    // (reversed columns rtop - j and rtop - j - 1, zero outside the image)
+    // (reversed columns rtop - j and rtop - j - 1, zero outside the image).
+    // Which items exist and where they sit in a row does not depend on the
+    // row: the column offsets and validity masks are fixed here, fetch_row
+    // only issues loads, and the loaded words are first touched by the next
+    // row's stage_row -- so each row's loads stay in flight for a whole row
+    // interval instead of being waited for where they are issued.
     uint64_t pa[STG], pb[STG];
+    int oa[STG], ob[STG];
+    bool ma[STG], mb[STG];
+#pragma unroll
+    for (int k = 0; k < STG; k++) {
+        const int i = kCost2Threads - 1 - tid + kCost2Threads * k;  // high waves: fewer pix columns
+        const bool left = i < nL;
+        const int xa = left ? ilo + i : rtop - (i - nL);
+        const int xb = xa - 1;
+        ma[k] = i < nItems && xa >= 0 && xa < W;
+        mb[k] = !left && i < nItems && xb >= 0 && xb < W;
+        const int pofs = left ? 0 : (int)plane;  // right plane follows the left one
+        oa[k] = pofs + clampi(xa, 0, W - 1);
+        ob[k] = pofs + clampi(xb, 0, W - 1);
+    }
     auto fetch_row = [&](int v) {
-        const int r = clampi(v, 0, H - 1);
-        const uint64_t* lrow = PL + (size_t)r * W;
-        const uint64_t* rrow = PR + (size_t)r * W;
+        const uint64_t* row = PL + (size_t)clampi(v, 0, H - 1) * W;
 #pragma unroll
         for (int k = 0; k < STG; k++) {
-            const int i = kCost2Threads - 1 - tid + kCost2Threads * k;  // high waves: fewer pix columns
-            const bool left = i < nL;
-            const int xa = left ? ilo + i : rtop - (i - nL);
-            const int xb = xa - 1;
-            const uint64_t* row = left ? lrow : rrow;
-            const bool oka = i < nItems && xa >= 0 && xa < W;
-            const bool okb = !left && i < nItems && xb >= 0 && xb < W;
-            const uint64_t va = row[clampi(xa, 0, W - 1)];
-            const uint64_t vb = row[clampi(xb, 0, W - 1)];
-            pa[k] = oka ? va : 0ull;
-            pb[k] = okb ? vb : 0ull;
+            pa[k] = row[oa[k]];
+            pb[k] = row[ob[k]];
         }
     };
     auto stage_row = [&](int buf) {
@@ -436,15 +444,16 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
         for (int k = 0; k < STG; k++) {
             const int i = kCost2Threads - 1 - tid + kCost2Threads * k;  // high waves: fewer pix columns
+            const uint64_t va = ma[k] ? pa[k] : 0ull, vb = mb[k] ? pb[k] : 0ull;
             if (i < nL) {
-                const uint3 fa = bt_bcast((uint32_t)pa[k]), fb = bt_bcast((uint32_t)(pa[k] >> 32));
+                const uint3 fa = bt_bcast((uint32_t)va), fb = bt_bcast((uint32_t)(va >> 32));
                 l4[i] = make_uint4(fa.x, fa.y, fa.z, fb.x);
                 l2[i] = make_uint2(fb.y, fb.z);
             } else if (i < nItems) {
                 const int j = i - nL;
                 const int q = (j & 1) * lay.qhalf + (j >> 1);
-                const uint3 fa = bt_pairform((uint32_t)pa[k], (uint32_t)pb[k]);
-                const uint3 fb = bt_pairform((uint32_t)(pa[k] >> 32), (uint32_t)(pb[k] >> 32));
+                const uint3 fa = bt_pairform((uint32_t)va, (uint32_t)vb);
+                const uint3 fb = bt_pairform((uint32_t)(va >> 32), (uint32_t)(vb >> 32));
                 q4[q] = make_uint4(fa.x, fa.y, fa.z, fb.x);
                 q2[q] = make_uint2(fb.y, fb.z);
             }
@@ -2078,7 +2087,7 @@ static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int
 {
     hipStream_t s = ctx->stream;
     int rc;
-    if (ctx->cost2 && e.SH2 <= 7) {
+    if (ctx->cost2 && e.SH2 <= 7 && e.SW2 == e.SH2) {
         const Cost2Layout l2 = cost2_layout(e.D, e.SW2, TY);
         const int items = 2 * l2.NX + e.D - 1;
         if (l2.CL >= 1 && items <= kCost2Threads * 2 &&
