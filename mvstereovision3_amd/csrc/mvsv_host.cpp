@@ -264,6 +264,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
         if (std::strstr(v, "path-wave")) c->path16 = 0;
         if (std::strstr(v, "path-lines")) c->tri = 0;
     }
+    if (const char* v = std::getenv("MVSV_COST_TY")) c->cost_ty = std::max(0, std::atoi(v));
     *out = c;
     return MVSV_OK;
 }

@@ -66,6 +66,7 @@ struct mvsv_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int path16 = 1;  // 16-lanes-per-scanline path kernels where D allows
     int cost2 = 1;   // register-ring cost kernel where blockSize <= 15
+    int cost_ty = 0;  // cost-volume tile height (0 = by image height); MVSV_COST_TY for A/B runs
     int tri = 1;     // sheared-strip kernels: three directions per sweep
     int lines_aux = 0;  // L->R line kernel on the second stream, beside the strip kernel
     // BM

@@ -321,7 +321,7 @@ constexpr int kCost2Threads = 512;
 constexpr int kCost2Run = 4;
 
 struct Cost2Layout {
-    int PP, CL, TX, TY, NX, nQmax, qhalf;
+    int PP, CL, TX, TY, NX, PS, nQmax, qhalf;
     size_t off_l4, off_l2, off_q4, off_q2, off_pix, bytes;
     size_t lstride4, lstride2, qstride4, qstride2, pstride;  // bytes per buffer (x2 each)
 };
@@ -338,14 +338,18 @@ __host__ __device__ inline Cost2Layout cost2_layout(int D, int SW2, int TY)
     c.CL = kCost2Threads / c.PP;
     c.TX = c.CL * kCost2Run;
     c.TY = TY;
-    c.NX = c.TX + 2 * SW2;
+    c.NX = c.TX + 2 * SW2;  // even
+    // pix row: [pair p][column], PS dwords per pair, PS = 2 (mod 64): the
+    // b64 column-pair stores (16-lane groups, 32 banks) and the b64 window
+    // loads (32-lane groups, 64 banks) of a wave are conflict-free
+    c.PS = c.NX + ((2 - c.NX) % 64 + 64) % 64;
     c.nQmax = c.NX + D - 1;
     c.qhalf = (c.nQmax + 1) / 2;  // slots per parity half
     c.lstride4 = (size_t)c.NX * 16;
     c.lstride2 = (size_t)c.NX * 8;
     c.qstride4 = (size_t)2 * c.qhalf * 16;
     c.qstride2 = (size_t)2 * c.qhalf * 8;
-    c.pstride = (size_t)c.NX * c.PP * 4;
+    c.pstride = (size_t)c.PS * c.PP * 4;
     c.off_l4 = 0;
     c.off_q4 = c.off_l4 + 2 * c.lstride4;
     c.off_l2 = c.off_q4 + 2 * c.qstride4;
@@ -403,8 +407,8 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
     const int tx0 = cl * kCost2Run;
     const uint32_t p2x2 = (uint32_t)(e.P2 & 0xffff) * 0x10001u;
     const int nItems = nL + nQ;
-    // no clamped columns in this tile and an even column-lane count
-    const bool linear = x0 - SW2 >= 0 && x0 + TX + SW2 <= W1 && (CL & 1) == 0;
+    // no clamped columns in this tile
+    const bool linear = x0 - SW2 >= 0 && x0 + TX + SW2 <= W1;
 
     // staging: item i < nL -> left column ilo + i; else right pair j = i - nL
     // (reversed columns rtop - j and rtop - j - 1, zero outside the image).
@@ -464,36 +468,46 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
         const uint2* l2 = (const uint2*)(smem + lay.off_l2 + buf * lay.lstride2);
         const uint4* q4 = (const uint4*)(smem + lay.off_q4 + buf * lay.qstride4);
         const uint2* q2 = (const uint2*)(smem + lay.off_q2 + buf * lay.qstride2);
-        uint32_t* pix = (uint32_t*)(smem + lay.off_pix + buf * lay.pstride);
+        uint32_t* prow = (uint32_t*)(smem + lay.off_pix + buf * lay.pstride) + p * lay.PS;
         if (!worker) return;
         // slot of right pair j = t + 2p (t = xchi - xc)
         auto qslot = [&](int t) { return (t & 1) * lay.qhalf + (t >> 1) + p; };
+        // column lane cl computes column pairs (xv, xv + 1), xv = 2 cl + 2 CL k,
+        // and stores each pair with one b64 write
         if (linear) {
-            // interior tile, CL even: column xv reads left slot xv and right
-            // slots qslot(nL - 1 - xv), which step by -CL/2 per iteration
-            const int t0 = nL - 1 - cl;
-            const int qs = qslot(t0), dq = CL >> 1;
-            const uint4* pl4 = l4 + cl;
-            const uint2* pl2 = l2 + cl;
-            const uint4* pq4 = q4 + qs;
-            const uint2* pq2 = q2 + qs;
-            uint32_t* pp = pix + cl * PP + p;
+            // interior tile: column xv reads left slot xv and right slot
+            // qslot(nL - 1 - xv); both step by a fixed amount per iteration
+            const int xa = 2 * cl;
+            const int ta = nL - 1 - xa;
+            const uint4* pl4 = l4 + xa;
+            const uint2* pl2 = l2 + xa;
+            const uint4* qa4 = q4 + qslot(ta);
+            const uint2* qa2 = q2 + qslot(ta);
+            const uint4* qb4 = q4 + qslot(ta - 1);
+            const uint2* qb2 = q2 + qslot(ta - 1);
+            uint2* pp = (uint2*)(prow + xa);
 #pragma unroll 1
-            for (int xv = cl; xv < NX; xv += CL) {
-                *pp = bt_cost2(*pl4, *pl2, *pq4, *pq2);
-                pl4 += CL;
-                pl2 += CL;
-                pq4 -= dq;
-                pq2 -= dq;
-                pp += CL * PP;
+            for (int xv = xa; xv < NX; xv += 2 * CL) {
+                const uint32_t c0 = bt_cost2(pl4[0], pl2[0], *qa4, *qa2);
+                const uint32_t c1 = bt_cost2(pl4[1], pl2[1], *qb4, *qb2);
+                *pp = make_uint2(c0, c1);
+                pl4 += 2 * CL;
+                pl2 += 2 * CL;
+                qa4 -= CL;
+                qa2 -= CL;
+                qb4 -= CL;
+                qb2 -= CL;
+                pp += CL;
             }
             return;
         }
 #pragma unroll 1
-        for (int xv = cl; xv < NX; xv += CL) {
-            const int xc0 = clampi(x0 - SW2 + xv, 0, W1 - 1) - xclo;
-            const int j0 = qslot(nL - 1 - xc0);
-            pix[xv * PP + p] = bt_cost2(l4[xc0], l2[xc0], q4[j0], q2[j0]);
+        for (int xv = 2 * cl; xv < NX; xv += 2 * CL) {
+            const int xca = clampi(x0 - SW2 + xv, 0, W1 - 1) - xclo;
+            const int xcb = clampi(x0 - SW2 + xv + 1, 0, W1 - 1) - xclo;
+            const int ja = qslot(nL - 1 - xca), jb = qslot(nL - 1 - xcb);
+            *(uint2*)(prow + xv) = make_uint2(bt_cost2(l4[xca], l2[xca], q4[ja], q2[ja]),
+                                              bt_cost2(l4[xcb], l2[xcb], q4[jb], q2[jb]));
         }
     };
 
@@ -529,16 +543,25 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
             pix_row(buf);
             __syncthreads();  // pix[buf] complete; staging of row k+1 visible
             if (worker) {
-                const uint32_t* pr =
-                    (const uint32_t*)(smem + lay.off_pix + buf * lay.pstride) + tx0 * PP + p;
+                // the thread's NR + RUN - 1 window columns: b64 loads, all in flight
+                constexpr int NV = NR + kCost2Run - 1;  // even
+                const uint2* pr = (const uint2*)((const uint32_t*)(smem + lay.off_pix + buf * lay.pstride) +
+                                                 p * lay.PS + tx0);
+                uint32_t wv[NV];
+#pragma unroll
+                for (int q = 0; q < NV / 2; q++) {
+                    const uint2 t2 = pr[q];
+                    wv[2 * q] = t2.x;
+                    wv[2 * q + 1] = t2.y;
+                }
                 uint32_t h = 0;
-                for (int q = 0; q <= 2 * SW2; q++) h = pk_add_u16(h, pr[q * PP]);
+#pragma unroll
+                for (int q = 0; q < NR; q++) h = pk_add_u16(h, wv[q]);
                 const bool emit = k >= NR - 1;
                 uint32_t* orow = obase + (size_t)k * ostride;
 #pragma unroll
                 for (int i = 0; i < kCost2Run; i++) {
-                    if (i > 0)
-                        h = pk_sub_u16(pk_add_u16(h, pr[(i + 2 * SW2) * PP]), pr[(i - 1) * PP]);
+                    if (i > 0) h = pk_sub_u16(pk_add_u16(h, wv[i + NR - 1]), wv[i - 1]);
                     csum[i] = pk_add_u16(pk_sub_u16(csum[i], ring[s][i]), h);
                     ring[s][i] = h;
                     if (emit && i < nout) orow[i * PP] = pk_add_u16(p2x2, csum[i]);
@@ -2186,7 +2209,19 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     }
 
     // cost volume: one block per TX x TY tile; keep the LDS image <= 160 KiB
-    int TY = H >= 512 ? 96 : (H >= 256 ? 48 : 16);
+    // Taller tiles re-read fewer halo rows (2*SH2 per tile); shorter ones give
+    // small batches enough blocks (>= 2 per CU) to fill the chip.
+    int TY = 16;
+    if (ctx->cost_ty > 0) {
+        TY = ctx->cost_ty;
+    } else if (H >= 256) {
+        const int TX = cost2_layout(e.D, e.SW2, 120).TX;
+        const long tiles_x = (e.W1 + TX - 1) / TX;
+        for (int ty : {120, 96, 64, 48}) {
+            TY = ty;
+            if (tiles_x * ((H + ty - 1) / ty) * n >= 512) break;
+        }
+    }
     if ((rc = launch_cost(ctx, n, W, H, e, TY, pre, Cv))) return rc;
 
     const int ybot = std::max(H - e.SH2, 1);     // first row that is never recomputed
