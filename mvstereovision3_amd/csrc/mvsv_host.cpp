@@ -265,6 +265,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
         if (std::strstr(v, "path-lines")) c->tri = 0;
     }
     if (const char* v = std::getenv("MVSV_COST_TY")) c->cost_ty = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("MVSV_LINES_AUX")) c->lines_aux = std::max(0, std::min(2, std::atoi(v)));
     *out = c;
     return MVSV_OK;
 }

@@ -957,6 +957,34 @@ __device__ __forceinline__ void sgm_step_row(const uint32_t (&lp)[NP], uint32_t 
     }
 }
 
+// sgm_step_row that also returns t = sat(m - delta) = delta_r - P2 in [-P2, 0]
+// (delta_r = the path's increment over cb, exact: every candidate of m lies
+// in [minLp, minLp + P2]).  The neighbour minima min(L[d-1], L[d+1]) of the
+// NP pairs come from NP + 1 pairwise minima X_q = min(pair q, pair q + 1):
+// pair p's is (X_{p-1}.hi, X_p.lo) -- one v_pk_min + one v_alignbit per pair.
+template <int NP>
+__device__ __forceinline__ void sgm_step_row_t(const uint32_t (&lp)[NP], uint32_t delta2,
+                                               uint32_t p1x2, const uint32_t (&c)[NP],
+                                               uint32_t (&ln)[NP], uint32_t (&t)[NP])
+{
+    const uint32_t MAXP = 0x7fff7fffu;
+    const uint32_t prev_hi = row_shr1(lp[NP - 1], MAXP);
+    const uint32_t next_lo = row_shl1(lp[0], MAXP);
+    uint32_t X[NP + 1];  // X[q + 1] = X_q, X[0] = X_{-1}
+    X[0] = pk_min(prev_hi, lp[0]);
+#pragma unroll
+    for (int q = 0; q + 1 < NP; q++) X[q + 1] = pk_min(lp[q], lp[q + 1]);
+    X[NP] = pk_min(lp[NP - 1], next_lo);
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+        const uint32_t nb = __builtin_amdgcn_alignbit(X[p + 1], X[p], 16);
+        uint32_t m = pk_min(lp[p], pk_add_sat(nb, p1x2));
+        m = pk_min(m, delta2);
+        t[p] = pk_sub_sat(m, delta2);
+        ln[p] = pk_add_sat(t[p], c[p]);
+    }
+}
+
 template <int NP>
 __device__ __forceinline__ int lane_min_row(const uint32_t (&ln)[NP])
 {
@@ -1030,14 +1058,14 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
     auto body = [&](int s, int j) {
         const int dl = (int16_t)(minp + P2);
         const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
-        uint32_t c[NP], ln[NP], o[NP];
+        uint32_t c[NP], ln[NP], o[NP], tt[NP];
 #pragma unroll
         for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
-        sgm_step_row<NP>(lp, delta2, p1x2, c, ln);
+        sgm_step_row_t<NP>(lp, delta2, p1x2, c, ln, tt);
         minp = row_min_i32(lane_min_row<NP>(ln));
 #pragma unroll
         for (int p = 0; p < NP; p++) {
-            uint32_t dv = path_delta(ln[p], c[p], p2x2);
+            const uint32_t dv = pk_add_u16(tt[p], p2x2);  // delta = t + P2
             o[p] = FIRST ? dv : AV::add(ab[j][p], dv);
             lp[p] = ln[p];
         }
@@ -1196,7 +1224,6 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     AccT* Af = A + f * frame + d0;
     AccT* dp = dummy + (size_t)threadIdx.x * 2 * NP;
     const uint32_t p1x2 = (uint32_t)(P1 & 0xffff) * 0x10001u;
-    // -3 * (C - P2) = C * 0xFFFD + 3 * P2 (mod 2^16)
     const uint32_t p2x3 = (uint32_t)((3 * P2) & 0xffff) * 0x10001u;
     const unsigned tag16 = epoch & 0xffffu;
     const unsigned long long tag = (unsigned long long)tag16 << 48;
@@ -1341,10 +1368,10 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
                 }
             }
             const int mb = *mcol(prv, 0, col + 1), mc = *mcol(prv, 1, col + 2);
-            uint32_t na[NP], nb[NP], nc[NP];
-            sgm_step_row<NP>(la, (uint32_t)((ma + P2) & 0xffff) * 0x10001u, p1x2, c, na);
-            sgm_step_row<NP>(pb, (uint32_t)((mb + P2) & 0xffff) * 0x10001u, p1x2, c, nb);
-            sgm_step_row<NP>(pc, (uint32_t)((mc + P2) & 0xffff) * 0x10001u, p1x2, c, nc);
+            uint32_t na[NP], nb[NP], nc[NP], ta[NP], tb_[NP], tc[NP];
+            sgm_step_row_t<NP>(la, (uint32_t)((ma + P2) & 0xffff) * 0x10001u, p1x2, c, na, ta);
+            sgm_step_row_t<NP>(pb, (uint32_t)((mb + P2) & 0xffff) * 0x10001u, p1x2, c, nb, tb_);
+            sgm_step_row_t<NP>(pc, (uint32_t)((mc + P2) & 0xffff) * 0x10001u, p1x2, c, nc, tc);
             const int mna = row_min_i32(lane_min_row<NP>(na));
             // the b and c minima share one packed row reduction (values <= 32767)
             const uint32_t mbc = row_min_u16x2((uint32_t)lane_min_row<NP>(nb) |
@@ -1352,9 +1379,8 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
             uint32_t o[NP];
 #pragma unroll
             for (int p = 0; p < NP; p++) {
-                // sum of the three deltas L - (C - P2), exact in u16 wrap arithmetic
-                const uint32_t c3n = pk_mad_u16(c[p], 0xfffdfffdu, p2x3);  // 3 * P2 - 3 * C
-                o[p] = pk_add_u16(pk_add_u16(na[p], nb[p]), pk_add_u16(nc[p], c3n));
+                // sum of the three deltas t_r + P2, exact in u16 wrap arithmetic
+                o[p] = pk_add_u16(pk_add_u16(ta[p], tb_[p]), pk_add_u16(tc[p], p2x3));
             }
             AV::store(valid ? Af + cell_off(t) : dp, o);
             if (__builtin_expect(!__all(valid), 0)) {
@@ -1568,10 +1594,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     auto body = [&](int s, int j) {
         const int dl = (int16_t)(minp + e.P2);
         const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
-        uint32_t c[NP], ln[NP], st[NP], acc[NP], w[NW];
+        uint32_t c[NP], ln[NP], st[NP], acc[NP], w[NW], tt[NP];
 #pragma unroll
         for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
-        sgm_step_row<NP>(lp, delta2, p1x2, c, ln);
+        sgm_step_row_t<NP>(lp, delta2, p1x2, c, ln, tt);
         minp = row_min_i32(lane_min_row<NP>(ln));
 #pragma unroll
         for (int k = 0; k < NW; k++) {
@@ -1995,13 +2021,15 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
             hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT>), grid, dim3(256), 0, ls, Cv,
                                Av + npass * plane, dummy, H, e.W1, e.D, 1, 0, e.P1, e.P2);
         };
-        if (ctx->lines_aux) lines();
+        // lines_aux: 0 = after the strip kernel on the same stream, 1 = on the
+        // second stream launched before it, 2 = on the second stream after it
+        if (ctx->lines_aux == 1) lines();
         if ((rc = check_hip(ctx, hipGetLastError(), "sgbm L->R lines"))) return rc;
         {
             StageTimer ts(ctx, kStageStrips);
             if ((rc = launch_tri<NP, AccT>(ctx, n, H, e, Cv, Av, plane, npass))) return rc;
         }
-        if (!ctx->lines_aux) lines();
+        if (ctx->lines_aux != 1) lines();
         if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_join, ctx->aux), "join")) ||
             (rc = check_hip(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0), "join wait")))
             return rc;
