@@ -56,7 +56,8 @@ def parse():
 def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True):
     """Algorithmic HBM bytes of one step per stage ("Kernels").
 
-    acc = bytes per (pixel, disparity) of a path-delta accumulator plane (1 when
+    acc = bytes per (pixel, disparity) of a path-delta accumulator plane (0.5 for
+    the 4-bit planes of the strip schedule when 3 * P2 <= 15, 1 when
     ndir * P2 <= 255, else 2).  strips = the sheared-strip schedule (D in
     {32, 64, 128, 256}): the strip kernel runs npass passes (down, + up for 8
     paths) that each read C and write their own plane, the L->R line kernel
@@ -147,7 +148,9 @@ def main():
     ndir = 8 if args.mode == 1 else 5
     P1 = params["p1"] if params["p1"] > 0 else 2
     P2 = max(params["p2"] if params["p2"] > 0 else 5, P1 + 1)
-    acc = 1 if ndir * P2 <= 255 else 2
+    # bytes per (pixel, disparity) of an accumulator plane: 4-bit planes on the
+    # strip schedule when 3 * P2 <= 15 (sgbm.yml: P2 = 5), else u8 / u16
+    acc = 0.5 if (D in (32, 64, 128, 256) and 3 * P2 <= 15) else (1 if ndir * P2 <= 255 else 2)
 
     from mvstereovision3_amd.batch import FrameBatch, frame_seeds
     host = [mvsv.synth_pair(sd, W, H, minD, D) for sd in frame_seeds(rank, world, F, SEED0)]
@@ -197,7 +200,7 @@ def main():
         kernels = [k for k in stages if not (k == "path_aggregation" and "path_strips" in stages)]
         dom = max(kernels, key=lambda k: stages[k]["ms_per_step"])
         launches = stages[dom]["launches_per_step"]
-        bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir, acc, strips) / launches
+        bytes_per_launch = int(stage_bytes(dom, F, W, H, W1, D, ndir, acc, strips) / launches)
         avg_launch_s = stages[dom]["ms_per_step"] / launches / 1e3
         achieved = bytes_per_launch / avg_launch_s / 1e9
         traffic = None

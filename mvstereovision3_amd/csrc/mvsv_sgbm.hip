@@ -614,6 +614,34 @@ __host__ __device__ inline bool acc_is_u8(const SgbmEff& e)
     return (e.fullDP ? 8 : 5) * e.P2 <= 255;
 }
 
+// 4-bit accumulator planes: the sheared-strip schedule writes one plane per
+// group of at most three directions (3 strip directions, or the L->R line),
+// so each plane holds sums <= 3 * P2; with P2 <= 5 (OpenCV's default P2 = 5,
+// which configs/sgbm.yml gets because it leaves P1/P2 at 0) they fit a nibble.
+// Element offsets stay in disparity units; a byte holds two of them.
+struct nib2_t {
+    uint8_t v;
+};
+__host__ __device__ inline bool acc_is_nib(const SgbmEff& e) { return 3 * e.P2 <= 15; }
+template <typename T>
+struct AccEpu {
+    static constexpr int v = 1;  // accumulator elements per storage unit
+};
+template <>
+struct AccEpu<nib2_t> {
+    static constexpr int v = 2;
+};
+template <>
+struct AccEpu<const nib2_t> {
+    static constexpr int v = 2;
+};
+template <typename T>
+__host__ __device__ __forceinline__ T* acc_add(T* p, ptrdiff_t e)
+{
+    return p + e / AccEpu<T>::v;  // e is even for nib2_t (d0 and D are even)
+}
+static_assert(AccEpu<const nib2_t>::v == 2 && AccEpu<const uint8_t>::v == 1, "accumulator units");
+
 __device__ __forceinline__ Line line_geometry(int line, int dx, int dy, int W1, int H)
 {
     Line g;
@@ -840,6 +868,32 @@ struct AccVec<8, uint8_t> {
     static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) { return a + b; }
 };
 
+// nibble storage of a lane's 2*NP sums (each <= 15): per group of four pairs
+// one dword, pair p's low half in nibble p and its high half in nibble p + 4
+// (three v_lshl_or_b32); two pairs: nibbles p and p + 2 of a u16; one pair:
+// nibbles 0, 1 of a byte.  Only the strip/line writers and the final kernel's
+// AccRaw<NP, nib2_t> read this layout.
+template <int NP>
+struct AccVec<NP, nib2_t> {
+    static __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+    {
+        return a | (b << 4) | (c << 8) | (d << 12);
+    }
+    static __device__ __forceinline__ void store(nib2_t* p, const uint32_t (&v)[NP])
+    {
+        if constexpr (NP == 1) {
+            *(uint8_t*)p = (uint8_t)(v[0] | (v[0] >> 12));
+        } else if constexpr (NP == 2) {
+            const uint32_t w = v[0] | (v[1] << 4);
+            *(uint16_t*)p = (uint16_t)(w | (w >> 8));
+        } else if constexpr (NP == 4) {
+            *(uint32_t*)p = pack4(v[0], v[1], v[2], v[3]);
+        } else {
+            *(uint2*)p = make_uint2(pack4(v[0], v[1], v[2], v[3]), pack4(v[4], v[5], v[6], v[7]));
+        }
+    }
+};
+
 // delta = L - C + P2 (exact, in [0, P2]) for a packed pair
 __device__ __forceinline__ uint32_t path_delta(uint32_t ln, uint32_t c, uint32_t p2x2)
 {
@@ -1037,8 +1091,8 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
     const int d0 = rl * 2 * NP;
     const size_t off = f * frame + ((size_t)g.ys * W1 + g.xs) * D + d0;
     const int16_t* cp = C + off;
-    AccT* ap = A + off;
-    AccT* dp = dummy + (size_t)threadIdx.x * 2 * NP;
+    AccT* ap = acc_add(A, (ptrdiff_t)off);
+    AccT* dp = acc_add(dummy, (ptrdiff_t)threadIdx.x * 2 * NP);
     const int last = max(len - 1, 0);
     uint32_t lp[NP];
 #pragma unroll
@@ -1053,7 +1107,7 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
     for (int j = 0; j < PF; j++) {
         const ptrdiff_t t = min(j, last);
         cb[j].load(cp + t * step);
-        if (!FIRST) AV::load(ap + t * step, ab[j]);
+        if constexpr (!FIRST) AV::load(acc_add(ap, t * step), ab[j]);
     }
     auto body = [&](int s, int j) {
         const int dl = (int16_t)(minp + P2);
@@ -1066,10 +1120,13 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
 #pragma unroll
         for (int p = 0; p < NP; p++) {
             const uint32_t dv = pk_add_u16(tt[p], p2x2);  // delta = t + P2
-            o[p] = FIRST ? dv : AV::add(ab[j][p], dv);
+            if constexpr (FIRST)
+                o[p] = dv;
+            else
+                o[p] = AV::add(ab[j][p], dv);
             lp[p] = ln[p];
         }
-        AccT* dst = s < len ? ap + (ptrdiff_t)s * step : dp;
+        AccT* dst = s < len ? acc_add(ap, (ptrdiff_t)s * step) : dp;
         AV::store(dst, o);
     };
     int s = 0;
@@ -1079,7 +1136,7 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
             body(s + j, j);
             const ptrdiff_t t = min(s + j + PF, last);
             cb[j].load(cp + t * step);
-            if (!FIRST) AV::load(ap + t * step, ab[j]);
+            if constexpr (!FIRST) AV::load(acc_add(ap, t * step), ab[j]);
         }
     }
     const int rem = maxlen - s;
@@ -1208,7 +1265,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     const int pass = chain / nframes;
     const int f = chain - pass * nframes;
     const int sy = pass == 0 ? 1 : -1;
-    A += pass * plane;
+    A = acc_add(A, (ptrdiff_t)pass * (ptrdiff_t)plane);
     const int Utot = W1 + H - 1;
     const int U0 = Utot - kTriSW * (k + 1);
     const int col = 4 * w + r;  // compute waves
@@ -1221,8 +1278,8 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     const int d0 = rl * 2 * NP;
     const size_t frame = (size_t)H * W1 * D;
     const int16_t* Cf = C + f * frame + d0;
-    AccT* Af = A + f * frame + d0;
-    AccT* dp = dummy + (size_t)threadIdx.x * 2 * NP;
+    AccT* Af = acc_add(A, (ptrdiff_t)(f * frame + d0));
+    AccT* dp = acc_add(dummy, (ptrdiff_t)threadIdx.x * 2 * NP);
     const uint32_t p1x2 = (uint32_t)(P1 & 0xffff) * 0x10001u;
     const uint32_t p2x3 = (uint32_t)((3 * P2) & 0xffff) * 0x10001u;
     const unsigned tag16 = epoch & 0xffffu;
@@ -1382,7 +1439,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
                 // sum of the three deltas t_r + P2, exact in u16 wrap arithmetic
                 o[p] = pk_add_u16(pk_add_u16(ta[p], tb_[p]), pk_add_u16(tc[p], p2x3));
             }
-            AV::store(valid ? Af + cell_off(t) : dp, o);
+            AV::store(valid ? acc_add(Af, cell_off(t)) : dp, o);
             if (__builtin_expect(!__all(valid), 0)) {
 #pragma unroll
                 for (int p = 0; p < NP; p++) {
@@ -1472,6 +1529,18 @@ struct AccRaw<NP, uint8_t> {
 #pragma unroll
         for (int p = 0; p < NP; p++) v[p] = u8x2_to_u16x2(w[p >> 1], p & 1);
     }
+    template <int NACC>
+    static __device__ __forceinline__ void combine(const uint32_t (&w)[NACC][NW], uint32_t (&v)[NP])
+    {
+        uint32_t s[NW];
+#pragma unroll
+        for (int k = 0; k < NW; k++) {
+            s[k] = w[0][k];
+#pragma unroll
+            for (int i = 1; i < NACC; i++) s[k] = add(s[k], w[i][k]);
+        }
+        unpack(s, v);
+    }
 };
 template <int NP>
 struct AccRaw<NP, uint16_t> {
@@ -1488,6 +1557,66 @@ struct AccRaw<NP, uint16_t> {
     {
 #pragma unroll
         for (int p = 0; p < NP; p++) v[p] = w[p];
+    }
+    template <int NACC>
+    static __device__ __forceinline__ void combine(const uint32_t (&w)[NACC][NW], uint32_t (&v)[NP])
+    {
+        uint32_t s[NW];
+#pragma unroll
+        for (int k = 0; k < NW; k++) {
+            s[k] = w[0][k];
+#pragma unroll
+            for (int i = 1; i < NACC; i++) s[k] = add(s[k], w[i][k]);
+        }
+        unpack(s, v);
+    }
+};
+// Nibble planes (AccVec<NP, nib2_t> layout): the planes' sums exceed a
+// nibble, so each word is split into its even and odd nibbles as bytes
+// (E, O), the planes are added bytewise (<= NACC * 15), then spread to pairs.
+template <int NP>
+struct AccRaw<NP, nib2_t> {
+    static constexpr int NW = NP >= 4 ? NP / 4 : 1;
+    static __device__ __forceinline__ void load(const nib2_t* p, uint32_t (&w)[NW])
+    {
+        if constexpr (NP == 1) {
+            w[0] = *(const uint8_t*)p;
+        } else if constexpr (NP == 2) {
+            w[0] = *(const uint16_t*)p;
+        } else if constexpr (NP == 4) {
+            w[0] = *(const uint32_t*)p;
+        } else {
+            const uint2 t = *(const uint2*)p;
+            w[0] = t.x;
+            w[1] = t.y;
+        }
+    }
+    template <int NACC>
+    static __device__ __forceinline__ void combine(const uint32_t (&w)[NACC][NW], uint32_t (&v)[NP])
+    {
+        constexpr uint32_t M = 0x0f0f0f0fu;
+#pragma unroll
+        for (int k = 0; k < NW; k++) {
+            uint32_t E = w[0][k] & M, O = (w[0][k] >> 4) & M;
+#pragma unroll
+            for (int i = 1; i < NACC; i++) {
+                E += w[i][k] & M;
+                O += (w[i][k] >> 4) & M;
+            }
+            if constexpr (NP >= 4) {
+                // E bytes: lo0 lo2 hi0 hi2, O bytes: lo1 lo3 hi1 hi3
+                v[4 * k + 0] = E & 0x00ff00ffu;
+                v[4 * k + 1] = O & 0x00ff00ffu;
+                v[4 * k + 2] = (E >> 8) & 0x00ff00ffu;
+                v[4 * k + 3] = (O >> 8) & 0x00ff00ffu;
+            } else if constexpr (NP == 2) {
+                // E bytes: lo0 hi0, O bytes: lo1 hi1
+                v[0] = __builtin_amdgcn_perm(0u, E, 0x0c010c00u);
+                v[1] = __builtin_amdgcn_perm(0u, O, 0x0c010c00u);
+            } else {
+                v[0] = (E & 0xffu) | ((O & 0xffu) << 16);
+            }
+        }
     }
 };
 
@@ -1551,7 +1680,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     const int d0 = rl * 2 * NP;
     const size_t off = f * frame + ((size_t)y * W1 + (W1 - 1)) * D + d0;
     const int16_t* cp = C + off;
-    const AccT* sp = A + off;
+    const AccT* sp = acc_add(A, (ptrdiff_t)off);
     uint16_t* ms = srow + row * DR;
     uint32_t lp[NP];
 #pragma unroll
@@ -1579,7 +1708,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     auto prefetch = [&](int j, ptrdiff_t t) {
         cb[j].load(cp - t * D);
 #pragma unroll
-        for (int i = 0; i < NACC; i++) AR::load(sp - t * D + i * plane, ab[j][i]);
+        for (int i = 0; i < NACC; i++) AR::load(acc_add(sp, -t * D + (ptrdiff_t)i * (ptrdiff_t)plane), ab[j][i]);
     };
 #pragma unroll
     for (int j = 0; j < PF; j++) prefetch(j, min(j, W1 - 1));
@@ -1594,18 +1723,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     auto body = [&](int s, int j) {
         const int dl = (int16_t)(minp + e.P2);
         const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
-        uint32_t c[NP], ln[NP], st[NP], acc[NP], w[NW], tt[NP];
+        uint32_t c[NP], ln[NP], st[NP], acc[NP], tt[NP];
 #pragma unroll
         for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
         sgm_step_row_t<NP>(lp, delta2, p1x2, c, ln, tt);
         minp = row_min_i32(lane_min_row<NP>(ln));
-#pragma unroll
-        for (int k = 0; k < NW; k++) {
-            w[k] = ab[j][0][k];
-#pragma unroll
-            for (int i = 1; i < NACC; i++) w[k] = AR::add(w[k], ab[j][i][k]);
-        }
-        AR::unpack(w, acc);
+        AR::template combine<NACC>(ab[j], acc);
         uint32_t key = 0x7fffffffu;
 #pragma unroll
         for (int p = 0; p < NP; p++) {
@@ -2019,7 +2142,8 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
             StageTimer tl(ctx, kStageLines, ls);
             dim3 grid((num_lines(1, 0, e.W1, H) + 15) / 16, n);
             hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT>), grid, dim3(256), 0, ls, Cv,
-                               Av + npass * plane, dummy, H, e.W1, e.D, 1, 0, e.P1, e.P2);
+                               acc_add(Av, (ptrdiff_t)npass * (ptrdiff_t)plane), dummy, H, e.W1,
+                               e.D, 1, 0, e.P1, e.P2);
         };
         // lines_aux: 0 = after the strip kernel on the same stream, 1 = on the
         // second stream launched before it, 2 = on the second stream after it
@@ -2117,6 +2241,13 @@ template <int NP>
 int launch_paths16_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv,
                        void* Av, int16_t* raw)
 {
+    if (use_strips(ctx, e, H) && acc_is_nib(e)) {
+        int rc;
+        if ((rc = ensure(ctx, ctx->dummy, 512 * 16 * 2 * NP, "sgbm dummy slots"))) return rc;
+        if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
+        const size_t plane = (size_t)n * H * e.W1 * e.D;
+        return launch_paths_tri<NP, nib2_t>(ctx, n, H, W, e, Cv, (nib2_t*)Av, plane, raw);
+    }
     if (acc_is_u8(e)) return launch_paths16<NP, uint8_t>(ctx, n, H, W, e, Cv, (uint8_t*)Av, raw);
     return launch_paths16<NP, uint16_t>(ctx, n, H, W, e, Cv, (uint16_t*)Av, raw);
 }
@@ -2221,7 +2352,9 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     // accumulator planes: one per concurrently written direction group
     const bool wide16 = ctx->path16 && (e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256);
     const int nplanes = (wide16 && use_strips(ctx, e, H)) ? (e.fullDP ? 3 : 2) : 1;
-    if ((rc = ensure(ctx, ctx->agg, (size_t)nplanes * n * vol * (acc_is_u8(e) ? 1 : 2),
+    const bool nib = nplanes > 1 && acc_is_nib(e);  // 4-bit planes on the strip schedule
+    if ((rc = ensure(ctx, ctx->agg, nib ? (size_t)nplanes * n * vol / 2
+                                        : (size_t)nplanes * n * vol * (acc_is_u8(e) ? 1 : 2),
                      "sgbm path-delta accumulator")))
         return rc;
     if ((rc = ensure(ctx, ctx->raw, (size_t)n * plane * 2, "sgbm raw disparity"))) return rc;

@@ -107,6 +107,19 @@ def test_sgbm_block_sizes(gpu, mvsv, oracle, bs, D):
     assert np.array_equal(got, want), report(got, want)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("D,P2", [(32, 0), (64, 5), (128, 0), (256, 5), (64, 6), (128, 3)])
+def test_sgbm_accumulator_plane_formats(gpu, mvsv, oracle, mode, D, P2):
+    """Sheared-strip schedule: 4-bit planes when 3 * P2 <= 15 (P2 = 0 -> OpenCV's 5,
+    sgbm.yml's case), u8 planes above (P2 = 6), for every D the strip kernels cover."""
+    W = 420 if D == 256 else 300
+    L, R = mvsv.synth_pair(SEED0 + 13 * D + P2, W, 72, 0, D)
+    got, want = sgbm_both(mvsv, oracle, L, R, minDisparity=2, numDisparities=D, blockSize=7,
+                          P1=2 if P2 == 3 else 0, P2=P2, uniquenessRatio=10, speckleWindowSize=20,
+                          speckleRange=2, mode=mode)
+    assert np.array_equal(got, want), report(got, want)
+
+
 @pytest.mark.parametrize("D", [16, 512])
 def test_sgbm_staging_two_slots(gpu, mvsv, oracle, D):
     # shapes whose cost-kernel staging needs two items per thread
