@@ -57,20 +57,22 @@ __device__ __forceinline__ uint32_t row_shl1(uint32_t v, uint32_t edge)
 }
 
 // Minimum / maximum over each 16-lane row; every lane of the row gets the result.
+// bound_ctrl is set: these patterns never read outside the row, and with it
+// the compiler folds each DPP move into the min/max (v_min_i32_dpp).
 __device__ __forceinline__ int row_min_i32(int v)
 {
-    v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
-    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
-    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, false));  // row_half_mirror
-    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, false));  // row_mirror
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true));   // quad_perm [1,0,3,2]
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true));   // quad_perm [2,3,0,1]
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, true));  // row_half_mirror
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, true));  // row_mirror
     return v;
 }
 __device__ __forceinline__ int row_max_i32(int v)
 {
-    v = max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false));
-    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false));
-    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, false));
-    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, true));
     return v;
 }
 
@@ -78,10 +80,10 @@ __device__ __forceinline__ int row_max_i32(int v)
 // inside each 16-lane row, then the four row results through readlane.
 __device__ __forceinline__ int wave_min_i32(int v)
 {
-    v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
-    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
-    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, false));  // row_half_mirror
-    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, false));  // row_mirror
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true));   // quad_perm [1,0,3,2]
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true));   // quad_perm [2,3,0,1]
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, true));  // row_half_mirror
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, true));  // row_mirror
     int a = __builtin_amdgcn_readlane(v, 0);
     int b = __builtin_amdgcn_readlane(v, 16);
     int c = __builtin_amdgcn_readlane(v, 32);

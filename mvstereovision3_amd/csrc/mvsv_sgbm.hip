@@ -1430,9 +1430,9 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
             sgm_step_row_t<NP>(pb, (uint32_t)((mb + P2) & 0xffff) * 0x10001u, p1x2, c, nb, tb_);
             sgm_step_row_t<NP>(pc, (uint32_t)((mc + P2) & 0xffff) * 0x10001u, p1x2, c, nc, tc);
             const int mna = row_min_i32(lane_min_row<NP>(na));
-            // the b and c minima share one packed row reduction (values <= 32767)
-            const uint32_t mbc = row_min_u16x2((uint32_t)lane_min_row<NP>(nb) |
-                                               ((uint32_t)lane_min_row<NP>(nc) << 16));
+            // DPP-folded i32 row minima (v_min_i32_dpp): one op per butterfly step
+            const int mnb = row_min_i32(lane_min_row<NP>(nb));
+            const int mnc = row_min_i32(lane_min_row<NP>(nc));
             uint32_t o[NP];
 #pragma unroll
             for (int p = 0; p < NP; p++) {
@@ -1459,8 +1459,8 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
                 dc[p] = nc[p];
             }
             if (rl == 0) {
-                *mcol(cur, 0, col) = valid ? (int)(mbc & 0xffffu) : 0;
-                *mcol(cur, 1, col) = valid ? (int)(mbc >> 16) : 0;
+                *mcol(cur, 0, col) = valid ? mnb : 0;
+                *mcol(cur, 1, col) = valid ? mnc : 0;
             }
         }
         __syncthreads();
