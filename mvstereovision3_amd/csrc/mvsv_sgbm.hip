@@ -339,10 +339,10 @@ __host__ __device__ inline Cost2Layout cost2_layout(int D, int SW2, int TY)
     c.TX = c.CL * kCost2Run;
     c.TY = TY;
     c.NX = c.TX + 2 * SW2;  // even
-    // pix row: [pair p][column], PS dwords per pair, PS = 2 (mod 64): the
-    // b64 column-pair stores (16-lane groups, 32 banks) and the b64 window
-    // loads (32-lane groups, 64 banks) of a wave are conflict-free
-    c.PS = c.NX + ((2 - c.NX) % 64 + 64) % 64;
+    // pix row: [pair p][column], PS dwords per pair with PS/2 odd: the b64
+    // column-pair stores (16-lane groups, 32 banks) and the b64 window loads
+    // (32-lane groups, 64 banks) of a wave are conflict-free
+    c.PS = c.NX + ((2 - c.NX) % 4 + 4) % 4;
     c.nQmax = c.NX + D - 1;
     c.qhalf = (c.nQmax + 1) / 2;  // slots per parity half
     c.lstride4 = (size_t)c.NX * 16;
