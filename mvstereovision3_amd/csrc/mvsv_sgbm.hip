@@ -526,6 +526,9 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
     uint32_t* obase = (uint32_t*)C + (((size_t)f * H + y0) * W1 + x0 + tx0) * PP + p -
                       (size_t)(2 * SH2) * ostride;
     const int nout = min(kCost2Run, W1 - (x0 + tx0));
+    const bool hh_pin = e.fullDP != 0;  // the fix-up kernel's MODE_HH cases, done here
+    const bool fix_x0 = (e.variant & MVSV_VARIANT_FIRSTCOL_FIX) != 0;
+    const int ybot = max(H - SH2, 1);
     fetch_row(vstart);
     stage_row(0);
     if (nrows > 1) fetch_row(vstart + 1);
@@ -559,12 +562,18 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                 for (int q = 0; q < NR; q++) h = pk_add_u16(h, wv[q]);
                 const bool emit = k >= NR - 1;
                 uint32_t* orow = obase + (size_t)k * ostride;
+                // MODE_HH: OpenCV 3.4 leaves P2 in the rows it never recomputes
+                // (y >= H - SH2) and in column x = 0 of rows y >= 1
+                const int yo = y0 - 2 * SH2 + k;
+                const bool pin_row = hh_pin && yo >= ybot;
+                const bool pin_x0 = hh_pin && !fix_x0 && yo >= 1 && x0 + tx0 == 0;
 #pragma unroll
                 for (int i = 0; i < kCost2Run; i++) {
                     if (i > 0) h = pk_sub_u16(pk_add_u16(h, wv[i + NR - 1]), wv[i - 1]);
                     csum[i] = pk_add_u16(pk_sub_u16(csum[i], ring[s][i]), h);
                     ring[s][i] = h;
-                    if (emit && i < nout) orow[i * PP] = pk_add_u16(p2x2, csum[i]);
+                    const bool pin = pin_row || (i == 0 && pin_x0);
+                    if (emit && i < nout) orow[i * PP] = pin ? p2x2 : pk_add_u16(p2x2, csum[i]);
                 }
             }
         }
@@ -2265,8 +2274,9 @@ int launch_paths_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
 // Cost-volume launch: the register-ring kernel when blockSize <= 15 and the
 // tile fits, else the LDS-ring kernel.
 static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int TY,
-                       const uint64_t* pre, int16_t* Cv)
+                       const uint64_t* pre, int16_t* Cv, bool* pinned_hh)
 {
+    *pinned_hh = false;
     hipStream_t s = ctx->stream;
     int rc;
     if (ctx->cost2 && e.SH2 <= 7 && e.SW2 == e.SH2) {
@@ -2311,6 +2321,7 @@ static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int
                 hipLaunchKernelGGL(kern, grid2, dim3(kCost2Threads), l2.bytes, s, pre, W, H, e, TY,
                                    Cv);
             }
+            *pinned_hh = e.fullDP != 0;  // MODE_HH fix-up rows/column written by the kernel
             return check_hip(ctx, hipGetLastError(), "sgbm cost kernel");
         }
     }
@@ -2383,11 +2394,12 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
             if (tiles_x * ((H + ty - 1) / ty) * n >= 512) break;
         }
     }
-    if ((rc = launch_cost(ctx, n, W, H, e, TY, pre, Cv))) return rc;
+    bool pinned_hh = false;
+    if ((rc = launch_cost(ctx, n, W, H, e, TY, pre, Cv, &pinned_hh))) return rc;
 
     const int ybot = std::max(H - e.SH2, 1);     // first row that is never recomputed
     const int ylast = std::max(H - e.SH2 - 1, 0);  // last recomputed row
-    if (H > 1) {
+    if (H > 1 && !pinned_hh) {
         StageTimer tm(ctx, kStageFixup);
         hipLaunchKernelGGL(sgbm_cost_fixup_kernel, dim3(H - 1, n), dim3(256), 0, s, Cv, H, e,
                            ylast, ybot);
