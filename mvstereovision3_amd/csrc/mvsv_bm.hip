@@ -3,6 +3,7 @@
 // Replaces Disparity::bm (src/disparity.cpp:18-22) -> cv::StereoBM::compute
 // with a CV_16S output.  Pipeline:
 //   1. bm_xsobel_kernel     [OpenCV] prefilterXSobel: clipped x-Sobel on row pairs
+//      (bm_prefilter_norm_kernel for PREFILTER_NORMALIZED_RESPONSE: prefilterNorm)
 //   2. fill_kernel          everything FILTERED = (minDisparity - 1) * 16
 //   3. bm_match_kernel      16x16 output tile per 256-thread block: the left /
 //                           right prefiltered tiles are staged in LDS, column
@@ -58,6 +59,50 @@ __global__ __launch_bounds__(256) void bm_xsobel_kernel(const uint8_t* __restric
             v = (uint8_t)(clampi(g, -cap, cap) + cap);
         }
         o[x] = v;
+    }
+}
+
+// [OpenCV] prefilterNorm (PREFILTER_NORMALIZED_RESPONSE), one block per row:
+// vsum[x] = sum of the winsize rows around y (replicated borders, exact in 16
+// bits: <= 255 * 255), sum(x) = sum of vsum over the winsize columns around x
+// (replicated), val = ((4 c[x] + c[x-1] + c[x+1] + p[x] + n[x]) * scale_g -
+// sum * scale_s) >> 10 with c/p/n the current / previous / next row
+// (replicated), out = clamp(val, -ftzero, ftzero) + ftzero.  The row's vsum
+// lives in LDS with wsz2 replicated cells on either side.
+__global__ __launch_bounds__(256) void bm_prefilter_norm_kernel(const uint8_t* __restrict__ src,
+                                                                size_t ss, size_t sfs, int W, int H,
+                                                                int winsize, int ftzero,
+                                                                uint8_t* __restrict__ dst)
+{
+    extern __shared__ int vs[];  // W + 2 * wsz2 cells
+    const int y = blockIdx.x;
+    const int f = blockIdx.y;
+    const int wsz2 = winsize / 2;
+    const uint8_t* s = src + f * sfs;
+    uint8_t* o = dst + ((size_t)f * H + y) * W;
+    const int scale_g0 = winsize * winsize / 8;
+    const int scale_s = (1024 + scale_g0) / (scale_g0 * 2);
+    const int scale_g = scale_g0 * scale_s;
+    for (int x = threadIdx.x; x < W; x += blockDim.x) {
+        int v = 0;
+        for (int r = y - wsz2; r <= y + wsz2; r++) v += s[(size_t)clampi(r, 0, H - 1) * ss + x];
+        vs[wsz2 + x] = v;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < wsz2; k += blockDim.x) {
+        vs[k] = vs[wsz2];
+        vs[wsz2 + W + k] = vs[wsz2 + W - 1];
+    }
+    __syncthreads();
+    const uint8_t* prev = s + (size_t)max(y - 1, 0) * ss;
+    const uint8_t* curr = s + (size_t)y * ss;
+    const uint8_t* next = s + (size_t)min(y + 1, H - 1) * ss;
+    for (int x = threadIdx.x; x < W; x += blockDim.x) {
+        int sum = 0;
+        for (int k = 0; k <= 2 * wsz2; k++) sum += vs[x + k];
+        const int c4 = curr[x] * 4 + curr[max(x - 1, 0)] + curr[min(x + 1, W - 1)];
+        const int val = ((c4 + prev[x] + next[x]) * scale_g - sum * scale_s) >> 10;
+        o[x] = (uint8_t)(clampi(val, -ftzero, ftzero) + ftzero);
     }
 }
 
@@ -267,16 +312,27 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
     if ((rc = check_hip(ctx, hipGetLastError(), "bm fill"))) return rc;
     if (e.lofs >= W || e.rofs >= W || e.width1 < 1) return MVSV_OK;
     if (e.xmax - e.xmin <= 0 || e.ymax - e.ymin <= 0 || e.ncol <= 0) return MVSV_OK;
-    if (e.prefilter_type != MVSV_PREFILTER_XSOBEL)
-        return set_error(ctx, MVSV_E_INVALID_ARG,
-                         "PREFILTER_NORMALIZED_RESPONSE is not implemented on the GPU path yet");
     const size_t plane = (size_t)W * H;
     if ((rc = ensure(ctx, ctx->bm_lf, (size_t)n * plane, "bm left prefilter"))) return rc;
     if ((rc = ensure(ctx, ctx->bm_rf, (size_t)n * plane, "bm right prefilter"))) return rc;
     uint8_t* Lf = (uint8_t*)ctx->bm_lf.ptr;
     uint8_t* Rf = (uint8_t*)ctx->bm_rf.ptr;
-    hipLaunchKernelGGL(bm_xsobel_kernel, dim3(H, n), dim3(256), 0, s, L, ls, lfs, W, H, e.cap, Lf);
-    hipLaunchKernelGGL(bm_xsobel_kernel, dim3(H, n), dim3(256), 0, s, R, rs, rfs, W, H, e.cap, Rf);
+    if (e.prefilter_type == MVSV_PREFILTER_XSOBEL) {
+        hipLaunchKernelGGL(bm_xsobel_kernel, dim3(H, n), dim3(256), 0, s, L, ls, lfs, W, H, e.cap, Lf);
+        hipLaunchKernelGGL(bm_xsobel_kernel, dim3(H, n), dim3(256), 0, s, R, rs, rfs, W, H, e.cap, Rf);
+    } else {
+        const size_t lds = (size_t)(W + e.prefilter_size) * sizeof(int);
+        if (lds > 160 * 1024) return set_error(ctx, MVSV_E_INVALID_ARG, "image too wide for the prefilter");
+        if (lds > 65536 &&
+            (rc = check_hip(ctx, hipFuncSetAttribute((const void*)bm_prefilter_norm_kernel,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                            "bm prefilter LDS attribute")))
+            return rc;
+        hipLaunchKernelGGL(bm_prefilter_norm_kernel, dim3(H, n), dim3(256), lds, s, L, ls, lfs, W, H,
+                           e.prefilter_size, e.cap, Lf);
+        hipLaunchKernelGGL(bm_prefilter_norm_kernel, dim3(H, n), dim3(256), lds, s, R, rs, rfs, W, H,
+                           e.prefilter_size, e.cap, Rf);
+    }
 
     const bool validate = e.disp12 >= 0;
     int* cost = nullptr;

@@ -253,6 +253,20 @@ def test_bm_config2_640x480(gpu, mvsv, oracle):
     assert np.array_equal(got, want), report(got, want)
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_bm_normalized_response_prefilter(gpu, mvsv, oracle, seed):
+    """StereoBM::PREFILTER_NORMALIZED_RESPONSE (prefilterNorm) on the GPU vs the oracle."""
+    rng = np.random.default_rng(3000 + seed)
+    H, W = int(rng.integers(40, 120)), int(rng.integers(80, 200))
+    p = bm_defaults(int(rng.choice([16, 32])), int(rng.choice([5, 9, 15])))
+    p.update(pre_filter_type=0, pre_filter_size=int(rng.choice([5, 7, 9, 21, 31])),
+             pre_filter_cap=int(rng.integers(1, 64)), min_disparity=int(rng.integers(-3, 3)),
+             texture_threshold=int(rng.choice([0, 10])), disp12_max_diff=int(rng.choice([-1, 1])))
+    L, R = rand_pair(rng, H, W, int(rng.integers(0, 12)), int(rng.integers(0, 3)))
+    got, want = bm_both(mvsv, oracle, L, R, p)
+    assert np.array_equal(got, want), f"{p}: " + report(got, want)
+
+
 def test_bm_validate_and_speckle(gpu, mvsv, oracle):
     L, R = mvsv.synth_pair(SEED0 + 23, 320, 200, 0, 48)
     p = bm_defaults(48, 11)
