@@ -1194,8 +1194,9 @@ struct TriLayout {
     static constexpr size_t kBytes = (size_t)(kLDw + kMinInts) * 4;
 };
 
-// Boundary granules of one strip and step: [3 items][16 lanes][NG] u64 (+ one
-// spare item row the comm wave's idle lanes store into).  Item 0 = L of dir
+// Boundary granules of one strip and step: [NG][4 item rows][16 lanes] u64
+// (the 4th item row is never written: the comm wave's spare lanes repeat
+// item 2).  Item 0 = L of dir
 // (0, sy) at the strip's first column, 1 = dir (-1, sy) at the first column,
 // 2 = dir (-1, sy) at the second column.  A lane's item is its 2*NP int16
 // costs + the column min, three int16 per granule under a 16-bit launch tag
@@ -1302,9 +1303,12 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     // zero both LDS rows (cells outside the image / before the first step)
     for (int i = threadIdx.x; i < TL::kLDw + TL::kMinInts; i += 64 * (kTriWaves + 1)) lds[i] = 0u;
 
-    // ---- comm wave: lanes (item j = min(r, 2), rl); row 3 duplicates item 2's
-    // loads and stores into the spare item row, so every comm-wave memory
-    // instruction is unpredicated and its wait counts are exact.
+    // ---- comm wave: lanes (item j = min(r, 2), rl); row 3 repeats item 2's
+    // loads and stores at item 2's own addresses (same values: the duplicate
+    // lanes cost no extra traffic), so every comm-wave memory instruction is
+    // unpredicated and its wait counts are exact.  A step's granules are laid
+    // out [granule i][item row][lane]: each of the NG store / load
+    // instructions covers 512 contiguous bytes.
     const int jj = min(r, 2);
     const bool jlive = r < 3;
     const int bcol = kTriSW + (jj == 2 ? 1 : 0);  // LDS column the consumed item lands in
@@ -1312,8 +1316,8 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     const int pcol = jj == 2 ? 1 : 0;              // own column published as item jj
     const size_t bstep = (size_t)4 * 16 * NG;
     const unsigned long long* bsrc =
-        bnd + tri_slot<NP>(chain, k > 0 ? k - 1 : k, 0, nchains, H) + ((size_t)jj * 16 + rl) * NG;
-    unsigned long long* pdst = bnd + tri_slot<NP>(chain, k, 0, nchains, H) + ((size_t)r * 16 + rl) * NG;
+        bnd + tri_slot<NP>(chain, k > 0 ? k - 1 : k, 0, nchains, H) + (size_t)jj * 16 + rl;
+    unsigned long long* pdst = bnd + tri_slot<NP>(chain, k, 0, nchains, H) + (size_t)jj * 16 + rl;
     auto bvalid = [&](int t) {
         const int xx = U0 + bcol - (H - 1) + t;
         return k > 0 && t >= 0 && xx >= 0 && xx < W1;
@@ -1321,7 +1325,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     auto bload = [&](int t, unsigned long long (&g)[NG]) {
         const unsigned long long* q = bsrc + (size_t)clampi(t, 0, H - 1) * bstep;
 #pragma unroll
-        for (int i = 0; i < NG; i++) g[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 0; i < NG; i++) g[i] = __hip_atomic_load(q + 64 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     // item t into LDS row buf, spinning until the producer's tag shows
     auto bconsume = [&](int t, int buf, unsigned long long (&g)[NG]) {
@@ -1346,7 +1350,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
                 ok = true;
 #pragma unroll
                 for (int i = 0; i < NG; i++) {
-                    g[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    g[i] = __hip_atomic_load(q + 64 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     ok &= !need || (unsigned)(g[i] >> 48) == tag16;
                 }
             }
@@ -1377,7 +1381,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
         TG::pack(v, mn, tag, g);
         unsigned long long* q = pdst + (size_t)clampi(t, 0, H - 1) * bstep;
 #pragma unroll
-        for (int i = 0; i < NG; i++) __hip_atomic_store(q + i, g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 0; i < NG; i++) __hip_atomic_store(q + 64 * i, g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
 
     // ---- compute waves ----
