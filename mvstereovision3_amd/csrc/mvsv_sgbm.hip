@@ -877,16 +877,17 @@ struct AccVec<8, uint8_t> {
     static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) { return a + b; }
 };
 
-// nibble storage of a lane's 2*NP sums (each <= 15): per group of four pairs
-// one dword, pair p's low half in nibble p and its high half in nibble p + 4
-// (three v_lshl_or_b32); two pairs: nibbles p and p + 2 of a u16; one pair:
-// nibbles 0, 1 of a byte.  Only the strip/line writers and the final kernel's
-// AccRaw<NP, nib2_t> read this layout.
+// nibble storage of the sums (each <= 15): every 4 consecutive disparities
+// d..d+3 = pairs (d, d+1), (d+2, d+3) form one u16 with d, d+2, d+1, d+3 in
+// nibbles 0..3 -- independent of how many pairs a lane holds, so writers with
+// 16 lanes per row and the final kernel's 32 lanes per row agree.  (One pair
+// per lane, D = 32 only: nibbles 0, 1 of a byte.)
 template <int NP>
 struct AccVec<NP, nib2_t> {
     static __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
     {
-        return a | (b << 4) | (c << 8) | (d << 12);
+        const uint32_t h0 = a | (b << 4), h1 = c | (d << 4);  // bytes 0 and 2 carry the groups
+        return __builtin_amdgcn_perm(h1, h0, 0x06040200u);
     }
     static __device__ __forceinline__ void store(nib2_t* p, const uint32_t (&v)[NP])
     {
@@ -1617,11 +1618,11 @@ struct AccRaw<NP, nib2_t> {
                 O += (w[i][k] >> 4) & M;
             }
             if constexpr (NP >= 4) {
-                // E bytes: lo0 lo2 hi0 hi2, O bytes: lo1 lo3 hi1 hi3
-                v[4 * k + 0] = E & 0x00ff00ffu;
-                v[4 * k + 1] = O & 0x00ff00ffu;
-                v[4 * k + 2] = (E >> 8) & 0x00ff00ffu;
-                v[4 * k + 3] = (O >> 8) & 0x00ff00ffu;
+                // E bytes: d0 d1 d4 d5, O bytes: d2 d3 d6 d7
+                v[4 * k + 0] = __builtin_amdgcn_perm(0u, E, 0x0c010c00u);
+                v[4 * k + 1] = __builtin_amdgcn_perm(0u, O, 0x0c010c00u);
+                v[4 * k + 2] = __builtin_amdgcn_perm(0u, E, 0x0c030c02u);
+                v[4 * k + 3] = __builtin_amdgcn_perm(0u, O, 0x0c030c02u);
             } else if constexpr (NP == 2) {
                 // E bytes: lo0 hi0, O bytes: lo1 hi1
                 v[0] = __builtin_amdgcn_perm(0u, E, 0x0c010c00u);
@@ -1632,6 +1633,51 @@ struct AccRaw<NP, nib2_t> {
         }
     }
 };
+
+// Lane segments of the final kernel: LPR lanes own one image row (16: a DPP
+// row; 32: two DPP rows joined by v_permlane16_swap).
+template <int LPR>
+__device__ __forceinline__ int seg_min_i32(int v)
+{
+    v = row_min_i32(v);
+    if constexpr (LPR == 32) {
+        const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+        v = min((int)sw[0], (int)sw[1]);
+    }
+    return v;
+}
+// sgm_step_row_t over an LPR-lane segment: the d-1 / d+1 neighbours of a lane's
+// first / last pair come from the adjacent lane of the segment (MAX at the
+// segment ends).
+template <int NP, int LPR>
+__device__ __forceinline__ void sgm_step_seg_t(const uint32_t (&lp)[NP], uint32_t delta2,
+                                               uint32_t p1x2, const uint32_t (&c)[NP],
+                                               uint32_t (&ln)[NP], uint32_t (&t)[NP], bool seg_first,
+                                               bool seg_last)
+{
+    if constexpr (LPR == 16) {
+        sgm_step_row_t<NP>(lp, delta2, p1x2, c, ln, t);
+    } else {
+        const uint32_t MAXP = 0x7fff7fffu;
+        const uint32_t ph = wave_shr1(lp[NP - 1], MAXP);
+        const uint32_t nl = wave_shl1(lp[0], MAXP);
+        const uint32_t prev_hi = seg_first ? MAXP : ph;
+        const uint32_t next_lo = seg_last ? MAXP : nl;
+        uint32_t X[NP + 1];  // X[q + 1] = X_q, X[0] = X_{-1}
+        X[0] = pk_min(prev_hi, lp[0]);
+#pragma unroll
+        for (int q = 0; q + 1 < NP; q++) X[q + 1] = pk_min(lp[q], lp[q + 1]);
+        X[NP] = pk_min(lp[NP - 1], next_lo);
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            const uint32_t nb = __builtin_amdgcn_alignbit(X[p + 1], X[p], 16);
+            uint32_t m = pk_min(lp[p], pk_add_sat(nb, p1x2));
+            m = pk_min(m, delta2);
+            t[p] = pk_sub_sat(m, delta2);
+            ln[p] = pk_add_sat(t[p], c[p]);
+        }
+    }
+}
 
 // Steps of C / accumulator prefetch: as deep as ~160 VGPRs of buffers allow
 // (a power of two dividing the 16-step flush period).  The kernel is bound by
@@ -1655,7 +1701,7 @@ __device__ __forceinline__ uint32_t pk_mad_u16_clamp(uint32_t a, uint32_t b, uin
 // NACC accumulator planes (A + i * plane) hold the summed deltas of disjoint
 // direction groups written by concurrent passes; their sum is the S input.
 // UQ: uniquenessRatio > 0.
-template <int NP, int NACC, typename AccT, bool UQ>
+template <int NP, int NACC, typename AccT, bool UQ, int LPR>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 : 2))) void sgbm_final16_kernel(const int16_t* __restrict__ C,
                                                          const AccT* __restrict__ A, size_t plane,
                                                          int H, int W, SgbmEff e,
@@ -1665,14 +1711,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
 {
     using AR = AccRaw<NP, AccT>;
     constexpr int NW = AR::NW;
-    constexpr int PF = final16_pf<NP, NACC, AccT, UQ>();
-    constexpr int DR = 32 * NP;  // disparities of a row (D)
+    // 32 lanes per row: twice the waves, so a shallower prefetch keeps the
+    // kernel at <= 128 VGPRs (4 waves per SIMD)
+    constexpr int PF = LPR == 32 ? 8 : final16_pf<NP, NACC, AccT, UQ>();
+    constexpr int RPW = 64 / LPR;     // image rows per wave
+    constexpr int DR = 2 * NP * LPR;  // disparities of a row (D)
     // S of the current step, one D-vector per row: S[best -+ 1] come back
     // through LDS instead of lane shuffles.
-    __shared__ __attribute__((aligned(16))) uint16_t srow[4 * DR];
+    __shared__ __attribute__((aligned(16))) uint16_t srow[RPW * DR];
     const int lane = threadIdx.x;
-    const int row = lane >> 4, rl = lane & 15;
-    const int yr = blockIdx.x * 4 + row;
+    const int row = lane / LPR, rl = lane % LPR;
+    const bool seg_first = rl == 0, seg_last = rl == LPR - 1;
+    const int yr = blockIdx.x * RPW + row;
     const bool exists = yr < H;
     const int y = min(yr, H - 1);
     const int f = blockIdx.y;
@@ -1681,7 +1731,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     int16_t* orow = raw + ((size_t)f * H + y) * W;
     uint32_t* krow = keys + ((size_t)f * H + y) * W;
     if (exists)
-        for (int x = rl; x < W; x += 16) {
+        for (int x = rl; x < W; x += LPR) {
             orow[x] = (int16_t)INV;
             krow[x] = 0xffffffffu;
         }
@@ -1731,16 +1781,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     // rl and the 16 lanes finish 16 columns at once (sub-pixel division, raw
     // store, right-view atomicMin) -- the per-step path stays branch-free so
     // consecutive steps overlap.
-    __shared__ uint2 srec[4 * 16];
-    uint2* recs = srec + row * 16;
+    __shared__ uint2 srec[RPW * LPR];
+    uint2* recs = srec + row * LPR;
     auto body = [&](int s, int j) {
         const int dl = (int16_t)(minp + e.P2);
         const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
         uint32_t c[NP], ln[NP], st[NP], acc[NP], tt[NP];
 #pragma unroll
         for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
-        sgm_step_row_t<NP>(lp, delta2, p1x2, c, ln, tt);
-        minp = row_min_i32(lane_min_row<NP>(ln));
+        sgm_step_seg_t<NP, LPR>(lp, delta2, p1x2, c, ln, tt, seg_first, seg_last);
+        minp = seg_min_i32<LPR>(lane_min_row<NP>(ln));
         AR::template combine<NACC>(ab[j], acc);
         uint32_t key = 0x7fffffffu;
 #pragma unroll
@@ -1753,7 +1803,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
             const uint32_t khi = (st[p] & 0xffff0000u) | subk[2 * p + 1];
             key = min(key, min(klo, khi));
         }
-        const int K = row_min_i32((int)key);
+        const int K = seg_min_i32<LPR>((int)key);
         const int minS = K >> 16;
         const int sub = K & 0xffff;
         const int best = lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
@@ -1779,10 +1829,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
                 const uint32_t lift = pk_sub_u16(pk_min_u16(yv, 0x00030003u), 0x00030003u);
                 m2 = pk_min_u16(m2, pk_max_u16(st[p], lift));
             }
-            const int m2r = row_min_i32((int)min(m2 & 0xffffu, m2 >> 16));
+            const int m2r = seg_min_i32<LPR>((int)min(m2 & 0xffffu, m2 >> 16));
             rej = m2r < 0xfffd && m2r * (100 - uq) < minS * 100;
         }
-        recs[s & 15] = make_uint2((uint32_t)K | ((uint32_t)rej << 31),
+        recs[s & (LPR - 1)] = make_uint2((uint32_t)K | ((uint32_t)rej << 31),
                                   ((uint32_t)Sp << 16) | ((uint32_t)Sm & 0xffffu));
         __builtin_amdgcn_wave_barrier();
     };
@@ -1817,17 +1867,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
                   hit ? (((uint32_t)minS << 16) | (uint32_t)(0xffff - x)) : 0xffffffffu);
     };
     int s = 0;
-    for (; s + 16 <= W1; s += 16) {
+    for (; s + LPR <= W1; s += LPR) {
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
+        for (int j = 0; j < LPR; j++) {
             body(s + j, j % PF);
             prefetch(j % PF, min(s + j + PF, W1 - 1));
         }
-        flush(s, 16);
+        flush(s, LPR);
     }
     const int rem = W1 - s;
 #pragma unroll
-    for (int j = 0; j < 16; j++) {
+    for (int j = 0; j < LPR; j++) {
         if (j < rem) {
             body(s + j, j % PF);
             prefetch(j % PF, min(s + j + PF, W1 - 1));
@@ -1838,7 +1888,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     __syncthreads();
     if (!exists) return;
     // left-right check (src: OpenCV 3.4 final loop) -- reads the finished row
-    for (int x = minX1 + rl; x < e.maxX1; x += 16) {
+    for (int x = minX1 + rl; x < e.maxX1; x += LPR) {
         const int v = orow[x];
         if (v == INV) continue;
         const int dlo = v >> kDispShift, dhi = (v + kDispScale - 1) >> kDispShift;
@@ -2048,14 +2098,21 @@ template <int NP, int NACC, typename AccT>
 void launch_final16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv,
                     const AccT* Av, size_t plane, int16_t* raw)
 {
+    // NP: disparity pairs per lane at 16 lanes per row.  D >= 128: 32 lanes per
+    // row (half the pairs per lane, twice the rows in flight per SIMD); a lane
+    // keeps >= 2 pairs, so it reads whole 4-disparity nibble groups.
+    constexpr int LPR = NP >= 4 ? 32 : 16;
+    constexpr int NPL = NP * 16 / LPR;
+    constexpr int RPW = 64 / LPR;
+    const dim3 grid((H + RPW - 1) / RPW, n);
     if (e.uniq > 0)
-        hipLaunchKernelGGL((sgbm_final16_kernel<NP, NACC, AccT, true>), dim3((H + 3) / 4, n),
-                           dim3(64), 0, ctx->stream, Cv, Av, plane, H, W, e, raw,
-                           (uint32_t*)ctx->keys.ptr, (int16_t*)ctx->dummy.ptr);
+        hipLaunchKernelGGL((sgbm_final16_kernel<NPL, NACC, AccT, true, LPR>), grid, dim3(64), 0,
+                           ctx->stream, Cv, Av, plane, H, W, e, raw, (uint32_t*)ctx->keys.ptr,
+                           (int16_t*)ctx->dummy.ptr);
     else
-        hipLaunchKernelGGL((sgbm_final16_kernel<NP, NACC, AccT, false>), dim3((H + 3) / 4, n),
-                           dim3(64), 0, ctx->stream, Cv, Av, plane, H, W, e, raw,
-                           (uint32_t*)ctx->keys.ptr, (int16_t*)ctx->dummy.ptr);
+        hipLaunchKernelGGL((sgbm_final16_kernel<NPL, NACC, AccT, false, LPR>), grid, dim3(64), 0,
+                           ctx->stream, Cv, Av, plane, H, W, e, raw, (uint32_t*)ctx->keys.ptr,
+                           (int16_t*)ctx->dummy.ptr);
 }
 
 static bool use_strips(const mvsv_ctx* ctx, const SgbmEff& e, int H)
