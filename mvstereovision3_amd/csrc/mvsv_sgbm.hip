@@ -1032,8 +1032,13 @@ __device__ __forceinline__ void sgm_step_row_t(const uint32_t (&lp)[NP], uint32_
                                                uint32_t (&ln)[NP], uint32_t (&t)[NP])
 {
     const uint32_t MAXP = 0x7fff7fffu;
-    const uint32_t prev_hi = row_shr1(lp[NP - 1], MAXP);
-    const uint32_t next_lo = row_shl1(lp[0], MAXP);
+    // d-1 / d+1 neighbours across the lane boundary: zero-filled DPP shifts
+    // (bound_ctrl) OR'ed with MAX at the row ends fold into v_or_b32_dpp
+    const uint32_t rl16 = __lane_id() & 15;
+    const uint32_t prev_hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)lp[NP - 1], 0x111, 0xf, 0xf, true) |
+                             (rl16 == 0 ? MAXP : 0u);
+    const uint32_t next_lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)lp[0], 0x101, 0xf, 0xf, true) |
+                             (rl16 == 15 ? MAXP : 0u);
     uint32_t X[NP + 1];  // X[q + 1] = X_q, X[0] = X_{-1}
     X[0] = pk_min(prev_hi, lp[0]);
 #pragma unroll
