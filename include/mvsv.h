@@ -214,6 +214,11 @@ MVSV_API int mvsv_stream_create(mvsv_ctx* ctx, int width, int height, const mvsv
                                 int depth, const mvsv_rect* grid_roi, mvsv_stream** out);
 /* new parameters for frames pushed from now on (the reference's setters between frames) */
 MVSV_API int mvsv_stream_set_params(mvsv_stream* s, const mvsv_sgbm_params* p);
+/* compute pushed frames `batch` at a time (1..depth, default 1): one frame-batch
+ * launch per group of consecutive frames -- the sustained rate of the batch
+ * kernels for up to batch-1 frames of extra latency; pop / set_params launch a
+ * partial group when they need its frames */
+MVSV_API int mvsv_stream_set_batch(mvsv_stream* s, int batch);
 /* MVSV_E_INVALID_ARG when depth frames are already pending (pop first) */
 MVSV_API int mvsv_stream_push(mvsv_stream* s, const uint8_t* left, size_t left_stride,
                               const uint8_t* right, size_t right_stride);

@@ -8,6 +8,12 @@
 // upload of frame i+1 (copy stream), the compute of frame i (context stream:
 // SGBM + the 9x9 mean grid of the ROI) and the download of frame i-1 (second
 // copy stream) overlap, and frames come back in push order.
+// With mvsv_stream_set_batch(b), pushed frames are computed b at a time: the
+// slots' device buffers are one contiguous [depth][frame] array, so a group of
+// consecutive slots is one frame-batch launch (sustained rate of the batch
+// kernels instead of the single-frame ones, at b frames of extra latency);
+// pop and set_params launch a partial group when they need to.
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -34,7 +40,12 @@ struct mvsv_stream {
         int status = MVSV_OK;
     };
     std::vector<Slot> slots;
-    long head = 0, tail = 0;  // pushed / popped frame counters
+    uint8_t *dL_all = nullptr, *dR_all = nullptr;  // [depth][H][W]
+    int16_t* dOut_all = nullptr;
+    float* dMeans_all = nullptr;  // [depth][81]
+    long head = 0, tail = 0;      // pushed / popped frame counters
+    long launched = 0;            // frames whose compute is enqueued
+    int batch = 1;
 };
 
 static void stream_free(mvsv_stream* st)
@@ -44,13 +55,13 @@ static void stream_free(mvsv_stream* st)
         if (s.hR) (void)hipHostFree(s.hR);
         if (s.hOut) (void)hipHostFree(s.hOut);
         if (s.hMeans) (void)hipHostFree(s.hMeans);
-        if (s.dL) (void)hipFree(s.dL);
-        if (s.dR) (void)hipFree(s.dR);
-        if (s.dOut) (void)hipFree(s.dOut);
-        if (s.dMeans) (void)hipFree(s.dMeans);
         for (hipEvent_t e : {s.uploaded, s.computed, s.done})
             if (e) (void)hipEventDestroy(e);
     }
+    if (st->dL_all) (void)hipFree(st->dL_all);
+    if (st->dR_all) (void)hipFree(st->dR_all);
+    if (st->dOut_all) (void)hipFree(st->dOut_all);
+    if (st->dMeans_all) (void)hipFree(st->dMeans_all);
     if (st->up) (void)hipStreamDestroy(st->up);
     if (st->down) (void)hipStreamDestroy(st->down);
     delete st;
@@ -83,15 +94,21 @@ int mvsv_stream_create(mvsv_ctx* ctx, int W, int H, const mvsv_sgbm_params* p, i
     bool ok = hipStreamCreateWithFlags(&st->up, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&st->down, hipStreamNonBlocking) == hipSuccess;
     st->slots.resize(depth);
-    for (auto& s : st->slots) {
+    ok = ok && hipMalloc((void**)&st->dL_all, px * depth) == hipSuccess &&
+         hipMalloc((void**)&st->dR_all, px * depth) == hipSuccess &&
+         hipMalloc((void**)&st->dOut_all, px * 2 * depth) == hipSuccess &&
+         hipMalloc((void**)&st->dMeans_all, 81 * sizeof(float) * depth) == hipSuccess;
+    for (size_t i = 0; i < st->slots.size(); i++) {
+        auto& s = st->slots[i];
         if (!ok) break;
+        s.dL = st->dL_all + i * px;
+        s.dR = st->dR_all + i * px;
+        s.dOut = st->dOut_all + i * px;
+        s.dMeans = st->dMeans_all + i * 81;
         ok = hipHostMalloc((void**)&s.hL, px, hipHostMallocDefault) == hipSuccess &&
              hipHostMalloc((void**)&s.hR, px, hipHostMallocDefault) == hipSuccess &&
              hipHostMalloc((void**)&s.hOut, px * 2, hipHostMallocDefault) == hipSuccess &&
              hipHostMalloc((void**)&s.hMeans, 81 * sizeof(float), hipHostMallocDefault) == hipSuccess &&
-             hipMalloc((void**)&s.dL, px) == hipSuccess && hipMalloc((void**)&s.dR, px) == hipSuccess &&
-             hipMalloc((void**)&s.dOut, px * 2) == hipSuccess &&
-             hipMalloc((void**)&s.dMeans, 81 * sizeof(float)) == hipSuccess &&
              hipEventCreateWithFlags(&s.uploaded, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&s.computed, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
@@ -105,6 +122,61 @@ int mvsv_stream_create(mvsv_ctx* ctx, int W, int H, const mvsv_sgbm_params* p, i
     return MVSV_OK;
 }
 
+// Enqueue compute + download for the pushed frames [launched, head): one
+// frame-batch launch per run of consecutive slots (a run ends at the ring's end).
+static int stream_launch(mvsv_stream* st)
+{
+    mvsv_ctx* ctx = st->ctx;
+    const int W = st->W, H = st->H;
+    const size_t px = (size_t)W * H;
+    const long depth = (long)st->slots.size();
+    int rc;
+    while (st->launched < st->head) {
+        const long i0 = st->launched % depth;
+        const int n = (int)std::min(st->head - st->launched, depth - i0);
+        auto& first = st->slots[i0];
+        auto& last = st->slots[i0 + n - 1];
+        // the upload stream is in order: the last slot's upload covers the run
+        if ((rc = check_hip(ctx, hipStreamWaitEvent(ctx->stream, last.uploaded, 0), "stream wait")))
+            return rc;
+        int status = sgbm_device(ctx, n, first.dL, W, px, first.dR, W, px, W, H, st->eff, first.dOut, W, px);
+        if (status == MVSV_OK && st->grid) {
+            const mvsv_rect& q = st->roi;
+            status = mean_grid_device(ctx, n, first.dOut + (size_t)q.y0 * W + q.x0, W, px, q.x1 - q.x0,
+                                      q.y1 - q.y0, first.dMeans);
+        }
+        if ((rc = check_hip(ctx, hipEventRecord(last.computed, ctx->stream), "stream event")) ||
+            (rc = check_hip(ctx, hipStreamWaitEvent(st->down, last.computed, 0), "stream wait")))
+            return rc;
+        for (int k = 0; k < n; k++) {
+            auto& s = st->slots[i0 + k];
+            s.status = status;
+            if ((rc = check_hip(ctx, hipMemcpyAsync(s.hOut, s.dOut, px * 2, hipMemcpyDeviceToHost, st->down),
+                                "stream D2H")))
+                return rc;
+            if (st->grid &&
+                (rc = check_hip(ctx, hipMemcpyAsync(s.hMeans, s.dMeans, 81 * sizeof(float),
+                                                    hipMemcpyDeviceToHost, st->down), "stream D2H")))
+                return rc;
+            if ((rc = check_hip(ctx, hipEventRecord(s.done, st->down), "stream event"))) return rc;
+        }
+        st->launched += n;
+    }
+    return MVSV_OK;
+}
+
+int mvsv_stream_set_batch(mvsv_stream* st, int batch)
+{
+    if (!st) return MVSV_E_INVALID_ARG;
+    if (batch < 1 || batch > (int)st->slots.size())
+        return set_error(st->ctx, MVSV_E_INVALID_ARG, "stream batch must be 1..depth");
+    (void)hipSetDevice(st->ctx->device);
+    int rc = stream_launch(st);  // frames already pushed keep the old grouping
+    if (rc) return rc;
+    st->batch = batch;
+    return MVSV_OK;
+}
+
 int mvsv_stream_set_params(mvsv_stream* st, const mvsv_sgbm_params* p)
 {
     if (!st) return MVSV_E_INVALID_ARG;
@@ -112,6 +184,8 @@ int mvsv_stream_set_params(mvsv_stream* st, const mvsv_sgbm_params* p)
     std::string why;
     int rc = resolve_sgbm(p, st->W, st->H, &e, &why);
     if (rc) return set_error(st->ctx, rc, why);
+    (void)hipSetDevice(st->ctx->device);
+    if ((rc = stream_launch(st))) return rc;  // pending frames keep the old parameters
     st->params = *p;  // applies to frames pushed from now on (trgt/mean_test.cpp:348 setters)
     st->eff = e;
     return MVSV_OK;
@@ -139,26 +213,12 @@ int mvsv_stream_push(mvsv_stream* st, const uint8_t* L, size_t ls, const uint8_t
     int rc;
     if ((rc = check_hip(ctx, hipMemcpyAsync(s.dL, s.hL, px, hipMemcpyHostToDevice, st->up), "stream H2D")) ||
         (rc = check_hip(ctx, hipMemcpyAsync(s.dR, s.hR, px, hipMemcpyHostToDevice, st->up), "stream H2D")) ||
-        (rc = check_hip(ctx, hipEventRecord(s.uploaded, st->up), "stream event")) ||
-        (rc = check_hip(ctx, hipStreamWaitEvent(ctx->stream, s.uploaded, 0), "stream wait")))
+        (rc = check_hip(ctx, hipEventRecord(s.uploaded, st->up), "stream event")))
         return rc;
-    s.status = sgbm_device(ctx, 1, s.dL, W, px, s.dR, W, px, W, H, st->eff, s.dOut, W, px);
-    if (s.status == MVSV_OK && st->grid) {
-        const mvsv_rect& q = st->roi;
-        s.status = mean_grid_device(ctx, 1, s.dOut + (size_t)q.y0 * W + q.x0, W, px, q.x1 - q.x0,
-                                    q.y1 - q.y0, s.dMeans);
-    }
-    if ((rc = check_hip(ctx, hipEventRecord(s.computed, ctx->stream), "stream event")) ||
-        (rc = check_hip(ctx, hipStreamWaitEvent(st->down, s.computed, 0), "stream wait")) ||
-        (rc = check_hip(ctx, hipMemcpyAsync(s.hOut, s.dOut, px * 2, hipMemcpyDeviceToHost, st->down),
-                        "stream D2H")))
-        return rc;
-    if (st->grid &&
-        (rc = check_hip(ctx, hipMemcpyAsync(s.hMeans, s.dMeans, 81 * sizeof(float),
-                                            hipMemcpyDeviceToHost, st->down), "stream D2H")))
-        return rc;
-    if ((rc = check_hip(ctx, hipEventRecord(s.done, st->down), "stream event"))) return rc;
     st->head++;
+    // a full group, or a group that would otherwise wrap past the ring's end
+    if (st->head - st->launched >= st->batch || st->head % (long)st->slots.size() == 0)
+        return stream_launch(st);
     return MVSV_OK;
 }
 
@@ -170,7 +230,9 @@ int mvsv_stream_pop(mvsv_stream* st, int16_t* out, size_t os, float* means)
     if (out && os < (size_t)st->W) return set_error(ctx, MVSV_E_INVALID_ARG, "stride smaller than width");
     auto& s = st->slots[st->tail % st->slots.size()];
     (void)hipSetDevice(ctx->device);
-    int rc = check_hip(ctx, hipEventSynchronize(s.done), "stream sync");
+    int rc = MVSV_OK;
+    if (st->tail >= st->launched && (rc = stream_launch(st))) return rc;  // partial group
+    rc = check_hip(ctx, hipEventSynchronize(s.done), "stream sync");
     st->tail++;
     if (rc) return rc;
     if (s.status) return s.status;

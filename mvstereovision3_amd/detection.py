@@ -197,10 +197,11 @@ class DisparityStream:
 
     push(left, right) uploads a rectified pair and enqueues SGBM (+ the 9x9
     mean grid of grid_roi); pop() returns (disparity int16, means[81] or None)
-    in push order.  `depth` frames may be in flight.
+    in push order.  `depth` frames may be in flight; with batch > 1 they are
+    computed in groups of `batch` frames (frame-batch kernels).
     """
 
-    def __init__(self, matcher, width, height, depth=3, grid_roi=None, device=0):
+    def __init__(self, matcher, width, height, depth=3, grid_roi=None, device=0, batch=1):
         self._ctx = context(device)
         self.width, self.height = width, height
         self._params = matcher._params
@@ -211,6 +212,12 @@ class DisparityStream:
                                        depth, ctypes.byref(roi) if roi is not None else None,
                                        ctypes.byref(h)), self._ctx.handle)
         self._h = h
+        if batch != 1:
+            self.set_batch(batch)
+
+    def set_batch(self, batch):
+        """Compute frames `batch` at a time (mvsv_stream_set_batch)."""
+        check(lib().mvsv_stream_set_batch(self._h, int(batch)), self._ctx.handle)
 
     def set_params(self, matcher):
         self._params = matcher._params

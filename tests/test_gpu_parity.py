@@ -430,6 +430,38 @@ def test_disparity_stream_matches_direct_compute(gpu, mvsv, oracle):
         assert np.array_equal(means, oracle.mean_disparity_grid(np.ascontiguousarray(want[y0:y1, x0:x1])))
 
 
+@pytest.mark.parametrize("depth,batch", [(4, 2), (5, 3), (6, 6)])
+def test_disparity_stream_batched(gpu, mvsv, oracle, depth, batch):
+    """Frames computed `batch` at a time: partial groups on pop, a parameter change
+    mid-group, groups cut at the slot ring's end -- every frame still matches."""
+    W, H, D = 256, 64, 64
+    m = mvsv.StereoSGBM.create(0, D, 7, 8 * 49, 32 * 49)
+    roi_u, _ = mvsv.create_dmap_rois((H, W), D)
+    st = mvsv.DisparityStream(m, W, H, depth=depth, grid_roi=roi_u, batch=batch)
+    frames = [mvsv.synth_pair(SEED0 + 60 + i, W, H, 0, D) for i in range(11)]
+    got, uq_from = [], 7
+    for i, (L, R) in enumerate(frames):
+        if st.pending() == depth or i in (3, 4):  # pops that force partial groups
+            got.append(st.pop())
+        if i == uq_from:
+            m.setUniquenessRatio(10)
+            st.set_params(m)
+        st.push(L, R)
+    while st.pending():
+        got.append(st.pop())
+    st.close()
+    assert len(got) == len(frames)
+    for i, ((L, R), (d, means)) in enumerate(zip(frames, got)):
+        p = dict(m.params())
+        p.pop("variant")
+        if i < uq_from:
+            p["uniqueness_ratio"] = 0
+        want = oracle.sgbm(L, R, p)
+        assert np.array_equal(d, want), f"frame {i}: " + report(d, want)
+        x0, y0, x1, y1 = roi_u
+        assert np.array_equal(means, oracle.mean_disparity_grid(np.ascontiguousarray(want[y0:y1, x0:x1])))
+
+
 # ----------------------------------------------------------- f2: remap -----
 def test_remap_matches_oracle(gpu, mvsv, oracle):
     import torch

@@ -6,10 +6,10 @@ on 1280x960 synthetic rectified pairs, followed by MeanDisparityDetection
 (build(MEAN_VALUE) on the createDMapROIS work ROI x in [128, W), detectObstacles)
 per frame -- the loop of trgt/mean_test.cpp:258-318 without its worker thread.
 Host frames go in, int16 maps and the 81 tile means come back (PCIe included);
-`depth` frames are in flight.  Also reports the device-resident rate of the same
+`depth` frames are in flight, computed `batch` at a time.  Also reports the device-resident rate of the same
 matcher on a batch of 8 frames.  Not the headline metric (bench.py is).
 
-    python tools/bench_stream.py [--frames 300] [--depth 3]
+    python tools/bench_stream.py [--frames 300] [--depth 16] [--batch 8]
 """
 import argparse
 import json
@@ -24,7 +24,8 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=300)
-    ap.add_argument("--depth", type=int, default=3)
+    ap.add_argument("--depth", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=8, help="frames per SGBM launch (mvsv_stream_set_batch)")
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=960)
     a = ap.parse_args()
@@ -44,7 +45,7 @@ def main():
     det.init((roi_u[3] - roi_u[1], roi_u[2] - roi_u[0]), Q, 0.1, 1.5)
     uniq = [mvsv.synth_pair(0x5EED0000 + i, W, H, 0, D) for i in range(8)]
 
-    st = mvsv.DisparityStream(m, W, H, depth=a.depth, grid_roi=roi_u)
+    st = mvsv.DisparityStream(m, W, H, depth=a.depth, grid_roi=roi_u, batch=a.batch)
     found = 0
 
     def consume():
@@ -85,7 +86,7 @@ def main():
     dwall = time.perf_counter() - t1
     print(json.dumps({
         "workload": f"config5_stream_{W}x{H}_d{D}_mode_sgbm",
-        "frames": a.frames, "depth": a.depth,
+        "frames": a.frames, "depth": a.depth, "batch": a.batch,
         "stream_fps": round(a.frames / wall, 2),
         "stream_mpix_s": round(a.frames * W * H / wall / 1e6, 2),
         "stream_ms_per_frame": round(wall / a.frames * 1e3, 3),
