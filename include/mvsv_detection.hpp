@@ -272,6 +272,8 @@ public:
     DisparityStream(const DisparityStream&) = delete;
     DisparityStream& operator=(const DisparityStream&) = delete;
     void setParams(const StereoSGBM& matcher) { check(mvsv_stream_set_params(s_, &matcher.params()), ctx_); }
+    // frames computed `batch` at a time (frame-batch kernels, up to batch-1 frames of latency)
+    void setBatch(int batch) { check(mvsv_stream_set_batch(s_, batch), ctx_); }
     int pending() const { return mvsv_stream_pending(s_); }
     void push(const Stereopair& s)
     {

@@ -44,6 +44,7 @@ int main(int argc, char** argv)
         mvsv::Mat Rm = mvsv::Mat::wrap(R.data(), 96, 320, mvsv::MAT_8UC1, 320);
         Stereopair s(Lm, Rm);
         mvsv::DisparityStream st(*sgbm, 320, 96, 2, &roi_u);
+        st.setBatch(2);  // both frames in one frame-batch launch
         st.push(s);
         st.push(s);
         mvsv::Mat d1, d2;
