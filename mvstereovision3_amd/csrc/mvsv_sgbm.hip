@@ -1408,6 +1408,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     unsigned long long bg[BF][NG];
 
     __syncthreads();  // LDS zeroed
+    if (comm) __builtin_amdgcn_s_setprio(1);  // the exchange wave gates every step's barrier
     if (comm) {
         bload(tb - 1, bg[0]);
         bconsume(tb - 1, 1, bg[0]);  // the right strip's cells the first step reads
