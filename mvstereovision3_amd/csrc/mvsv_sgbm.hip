@@ -380,7 +380,7 @@ __device__ __forceinline__ uint32_t bt_cost2(uint4 u4, uint2 u2, uint4 v4, uint2
     return pk_add_u16(ca, __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, cb) >> two));
 }
 
-template <int NR, int STG>
+template <int NR, int STG, int PPC>
 __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4))) void sgbm_cost2_kernel(const uint64_t* __restrict__ pre,
                                                                    int W, int H, SgbmEff e, int TY,
                                                                    int16_t* __restrict__ C)
@@ -390,7 +390,11 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
     constexpr int SW2 = SH2;  // StereoSGBM's window is square (SW = SH = blockSize)
     const int D = e.D, W1 = e.W1;
     const Cost2Layout lay = cost2_layout(D, SW2, TY);
-    const int PP = lay.PP, CL = lay.CL, TX = lay.TX, NX = lay.NX;
+    // PPC > 0: the disparity-pair count is known at compile time (PPC == D / 2),
+    // so the interior pixel-cost loop unrolls with every LDS address an
+    // immediate offset from one base per operand
+    const int PP = PPC > 0 ? PPC : lay.PP, CL = PPC > 0 ? kCost2Threads / PPC : lay.CL;
+    const int TX = CL * kCost2Run, NX = lay.NX;
     const int f = blockIdx.z;
     const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
     const int y1 = min(y0 + TY, H);
@@ -455,7 +459,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                 l2[i] = make_uint2(fb.y, fb.z);
             } else if (i < nItems) {
                 const int j = i - nL;
-                const int q = (j & 1) * lay.qhalf + (j >> 1);
+                const int q = (j & 1) * lay.qhalf + lay.qhalf - 1 - (j >> 1);  // descending
                 const uint3 fa = bt_pairform((uint32_t)va, (uint32_t)vb);
                 const uint3 fb = bt_pairform((uint32_t)(va >> 32), (uint32_t)(vb >> 32));
                 q4[q] = make_uint4(fa.x, fa.y, fa.z, fb.x);
@@ -470,8 +474,9 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
         const uint2* q2 = (const uint2*)(smem + lay.off_q2 + buf * lay.qstride2);
         uint32_t* prow = (uint32_t*)(smem + lay.off_pix + buf * lay.pstride) + p * lay.PS;
         if (!worker) return;
-        // slot of right pair j = t + 2p (t = xchi - xc)
-        auto qslot = [&](int t) { return (t & 1) * lay.qhalf + (t >> 1) + p; };
+        // slot of right pair j = t + 2p (t = xchi - xc); slots descend with j, so
+        // a column lane's slot ascends as its column xv does
+        auto qslot = [&](int t) { return (t & 1) * lay.qhalf + lay.qhalf - 1 - (t >> 1) - p; };
         // column lane cl computes column pairs (xv, xv + 1), xv = 2 cl + 2 CL k,
         // and stores each pair with one b64 write
         if (linear) {
@@ -479,6 +484,26 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
             // qslot(nL - 1 - xv); both step by a fixed amount per iteration
             const int xa = 2 * cl;
             const int ta = nL - 1 - xa;
+            if constexpr (PPC > 0) {
+                constexpr int CLC = kCost2Threads / PPC;
+                constexpr int KMAX = 2 + (SW2 + CLC - 1) / CLC;  // ceil((TX + 2 SW2) / (2 CL))
+                const uint4* pl4 = l4 + xa;
+                const uint2* pl2 = l2 + xa;
+                const uint4* qa4 = q4 + qslot(ta);
+                const uint2* qa2 = q2 + qslot(ta);
+                const uint4* qb4 = q4 + qslot(ta - 1);
+                const uint2* qb2 = q2 + qslot(ta - 1);
+                uint2* pp = (uint2*)(prow + xa);
+#pragma unroll
+                for (int k = 0; k < KMAX; k++) {
+                    if (xa + 2 * CLC * k >= NX) break;
+                    const uint32_t c0 = bt_cost2(pl4[2 * CLC * k], pl2[2 * CLC * k], qa4[CLC * k], qa2[CLC * k]);
+                    const uint32_t c1 =
+                        bt_cost2(pl4[2 * CLC * k + 1], pl2[2 * CLC * k + 1], qb4[CLC * k], qb2[CLC * k]);
+                    pp[CLC * k] = make_uint2(c0, c1);
+                }
+                return;
+            }
             const uint4* pl4 = l4 + xa;
             const uint2* pl2 = l2 + xa;
             const uint4* qa4 = q4 + qslot(ta);
@@ -493,10 +518,10 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                 *pp = make_uint2(c0, c1);
                 pl4 += 2 * CL;
                 pl2 += 2 * CL;
-                qa4 -= CL;
-                qa2 -= CL;
-                qb4 -= CL;
-                qb2 -= CL;
+                qa4 += CL;
+                qa2 += CL;
+                qb4 += CL;
+                qb2 += CL;
                 pp += CL;
             }
             return;
@@ -2354,27 +2379,28 @@ static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int
             dim3 grid2((e.W1 + l2.TX - 1) / l2.TX, (H + TY - 1) / TY, n);
             void (*kern)(const uint64_t*, int, int, SgbmEff, int, int16_t*) = nullptr;
             const bool two = items > kCost2Threads;
+            const bool pp64 = l2.PP == 64;
             if (!two) {
                 switch (2 * e.SH2 + 1) {
-                case 1: kern = sgbm_cost2_kernel<1, 1>; break;
-                case 3: kern = sgbm_cost2_kernel<3, 1>; break;
-                case 5: kern = sgbm_cost2_kernel<5, 1>; break;
-                case 7: kern = sgbm_cost2_kernel<7, 1>; break;
-                case 9: kern = sgbm_cost2_kernel<9, 1>; break;
-                case 11: kern = sgbm_cost2_kernel<11, 1>; break;
-                case 13: kern = sgbm_cost2_kernel<13, 1>; break;
-                default: kern = sgbm_cost2_kernel<15, 1>; break;
+                case 1: kern = pp64 ? sgbm_cost2_kernel<1, 1, 64> : sgbm_cost2_kernel<1, 1, 0>; break;
+                case 3: kern = pp64 ? sgbm_cost2_kernel<3, 1, 64> : sgbm_cost2_kernel<3, 1, 0>; break;
+                case 5: kern = pp64 ? sgbm_cost2_kernel<5, 1, 64> : sgbm_cost2_kernel<5, 1, 0>; break;
+                case 7: kern = pp64 ? sgbm_cost2_kernel<7, 1, 64> : sgbm_cost2_kernel<7, 1, 0>; break;
+                case 9: kern = pp64 ? sgbm_cost2_kernel<9, 1, 64> : sgbm_cost2_kernel<9, 1, 0>; break;
+                case 11: kern = pp64 ? sgbm_cost2_kernel<11, 1, 64> : sgbm_cost2_kernel<11, 1, 0>; break;
+                case 13: kern = pp64 ? sgbm_cost2_kernel<13, 1, 64> : sgbm_cost2_kernel<13, 1, 0>; break;
+                default: kern = pp64 ? sgbm_cost2_kernel<15, 1, 64> : sgbm_cost2_kernel<15, 1, 0>; break;
                 }
             } else {
                 switch (2 * e.SH2 + 1) {
-                case 1: kern = sgbm_cost2_kernel<1, 2>; break;
-                case 3: kern = sgbm_cost2_kernel<3, 2>; break;
-                case 5: kern = sgbm_cost2_kernel<5, 2>; break;
-                case 7: kern = sgbm_cost2_kernel<7, 2>; break;
-                case 9: kern = sgbm_cost2_kernel<9, 2>; break;
-                case 11: kern = sgbm_cost2_kernel<11, 2>; break;
-                case 13: kern = sgbm_cost2_kernel<13, 2>; break;
-                default: kern = sgbm_cost2_kernel<15, 2>; break;
+                case 1: kern = pp64 ? sgbm_cost2_kernel<1, 2, 64> : sgbm_cost2_kernel<1, 2, 0>; break;
+                case 3: kern = pp64 ? sgbm_cost2_kernel<3, 2, 64> : sgbm_cost2_kernel<3, 2, 0>; break;
+                case 5: kern = pp64 ? sgbm_cost2_kernel<5, 2, 64> : sgbm_cost2_kernel<5, 2, 0>; break;
+                case 7: kern = pp64 ? sgbm_cost2_kernel<7, 2, 64> : sgbm_cost2_kernel<7, 2, 0>; break;
+                case 9: kern = pp64 ? sgbm_cost2_kernel<9, 2, 64> : sgbm_cost2_kernel<9, 2, 0>; break;
+                case 11: kern = pp64 ? sgbm_cost2_kernel<11, 2, 64> : sgbm_cost2_kernel<11, 2, 0>; break;
+                case 13: kern = pp64 ? sgbm_cost2_kernel<13, 2, 64> : sgbm_cost2_kernel<13, 2, 0>; break;
+                default: kern = pp64 ? sgbm_cost2_kernel<15, 2, 64> : sgbm_cost2_kernel<15, 2, 0>; break;
                 }
             }
             if (l2.bytes > 65536 &&
