@@ -126,19 +126,36 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(const int16_t* __res
         lcnt[li] = 0;
     }
     __syncthreads();
+    // Horizontal runs without atomics: a wave holds two whole tile rows, so the
+    // ballot of "connected to the right neighbour" gives each lane its run's
+    // first pixel (the smallest index, so roots stay minimal), and every pixel
+    // links straight to it.
+    __shared__ unsigned hrow[kSpTile];  // bit x: (x, ly) -- (x + 1, ly) connected
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int ly = ty + 8 * k, li = ly * kSpTile + tx;
         const int v = lval[li];
-        if (v == kInvalid) continue;
-        if (tx + 1 < kSpTile) {
-            int u = lval[li + 1];
-            if (u != kInvalid && abs(v - u) <= max_diff) lunite(lpar, li, li + 1);
+        const int u = tx + 1 < kSpTile ? lval[li + 1] : kInvalid;
+        const bool h = v != kInvalid && u != kInvalid && abs(v - u) <= max_diff;
+        const unsigned hm = (unsigned)(__ballot(h) >> (lane & 32));
+        const unsigned starts = ~(hm << 1) & ((2u << tx) - 1u);  // run starts at or left of tx
+        lpar[li] = ly * kSpTile + 31 - __clz(starts);
+        if (tx == 0) hrow[ly] = hm;
+    }
+    __syncthreads();
+    // Vertical links join runs; of a stretch of vertical links between the same
+    // two runs only the leftmost one unites
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int ly = ty + 8 * k, li = ly * kSpTile + tx;
+        if (ly + 1 >= kSpTile) continue;
+        const int v = lval[li], u = lval[li + kSpTile];
+        if (v == kInvalid || u == kInvalid || abs(v - u) > max_diff) continue;
+        if (tx > 0 && ((hrow[ly] & hrow[ly + 1]) >> (tx - 1) & 1u)) {
+            const int vl = lval[li - 1], ul = lval[li + kSpTile - 1];
+            if (abs(vl - ul) <= max_diff) continue;  // both valid: h bits set
         }
-        if (ly + 1 < kSpTile) {
-            int u = lval[li + kSpTile];
-            if (u != kInvalid && abs(v - u) <= max_diff) lunite(lpar, li, li + kSpTile);
-        }
+        lunite(lpar, li, li + kSpTile);
     }
     __syncthreads();
     int root[4];

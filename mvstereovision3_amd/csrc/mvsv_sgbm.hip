@@ -445,10 +445,10 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
         }
     };
     auto stage_row = [&](int buf) {
-        uint4* l4 = (uint4*)(smem + lay.off_l4 + buf * lay.lstride4);
-        uint2* l2 = (uint2*)(smem + lay.off_l2 + buf * lay.lstride2);
-        uint4* q4 = (uint4*)(smem + lay.off_q4 + buf * lay.qstride4);
-        uint2* q2 = (uint2*)(smem + lay.off_q2 + buf * lay.qstride2);
+        uint4* l4 = (uint4*)(smem + lay.off_l4 + (buf ? lay.lstride4 : 0));
+        uint2* l2 = (uint2*)(smem + lay.off_l2 + (buf ? lay.lstride2 : 0));
+        uint4* q4 = (uint4*)(smem + lay.off_q4 + (buf ? lay.qstride4 : 0));
+        uint2* q2 = (uint2*)(smem + lay.off_q2 + (buf ? lay.qstride2 : 0));
 #pragma unroll
         for (int k = 0; k < STG; k++) {
             const int i = kCost2Threads - 1 - tid + kCost2Threads * k;  // high waves: fewer pix columns
@@ -468,11 +468,11 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
         }
     };
     auto pix_row = [&](int buf) {
-        const uint4* l4 = (const uint4*)(smem + lay.off_l4 + buf * lay.lstride4);
-        const uint2* l2 = (const uint2*)(smem + lay.off_l2 + buf * lay.lstride2);
-        const uint4* q4 = (const uint4*)(smem + lay.off_q4 + buf * lay.qstride4);
-        const uint2* q2 = (const uint2*)(smem + lay.off_q2 + buf * lay.qstride2);
-        uint32_t* prow = (uint32_t*)(smem + lay.off_pix + buf * lay.pstride) + p * lay.PS;
+        const uint4* l4 = (const uint4*)(smem + lay.off_l4 + (buf ? lay.lstride4 : 0));
+        const uint2* l2 = (const uint2*)(smem + lay.off_l2 + (buf ? lay.lstride2 : 0));
+        const uint4* q4 = (const uint4*)(smem + lay.off_q4 + (buf ? lay.qstride4 : 0));
+        const uint2* q2 = (const uint2*)(smem + lay.off_q2 + (buf ? lay.qstride2 : 0));
+        uint32_t* prow = (uint32_t*)(smem + lay.off_pix + (buf ? lay.pstride : 0)) + p * lay.PS;
         if (!worker) return;
         // slot of right pair j = t + 2p (t = xchi - xc); slots descend with j, so
         // a column lane's slot ascends as its column xv does
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
             if (worker) {
                 // the thread's NR + RUN - 1 window columns: b64 loads, all in flight
                 constexpr int NV = NR + kCost2Run - 1;  // even
-                const uint2* pr = (const uint2*)((const uint32_t*)(smem + lay.off_pix + buf * lay.pstride) +
+                const uint2* pr = (const uint2*)((const uint32_t*)(smem + lay.off_pix + (buf ? lay.pstride : 0)) +
                                                  p * lay.PS + tx0);
                 uint32_t wv[NV];
 #pragma unroll
