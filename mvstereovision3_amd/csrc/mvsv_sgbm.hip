@@ -1721,6 +1721,33 @@ constexpr int final16_pf()
     return budget / words >= 16 ? 16 : (budget / words >= 8 ? 8 : 4);
 }
 
+// raw buffer loads of BYTES bytes into little-endian words (zero-extended)
+constexpr int kBufWord3 = 0x00020000;  // buffer descriptor word 3: 32-bit data format
+template <int BYTES, int NWD>
+__device__ __forceinline__ void buf_words(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff,
+                                          uint32_t (&w)[NWD])
+{
+    if constexpr (BYTES == 1) {
+        w[0] = __builtin_amdgcn_raw_buffer_load_b8(r, voff, soff, 0);
+    } else if constexpr (BYTES == 2) {
+        w[0] = __builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0);
+    } else if constexpr (BYTES == 4) {
+        w[0] = __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+    } else if constexpr (BYTES == 8) {
+        const auto t = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+        w[0] = t[0];
+        w[1] = t[1];
+    } else {
+        static_assert(BYTES % 16 == 0 && NWD == BYTES / 4, "buffer load size");
+#pragma unroll
+        for (int q = 0; q < BYTES / 16; q++) {
+            const auto t = __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16 * q, soff, 0);
+#pragma unroll
+            for (int k = 0; k < 4; k++) w[4 * q + k] = t[k];
+        }
+    }
+}
+
 // a * b + c per u16 half, saturated at 0xffff (VOP3P clamp)
 __device__ __forceinline__ uint32_t pk_mad_u16_clamp(uint32_t a, uint32_t b, uint32_t c)
 {
@@ -1799,10 +1826,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
 
     Vec<NP> cb[PF];
     uint32_t ab[PF][NACC][NW];
-    auto prefetch = [&](int j, ptrdiff_t t) {
-        cb[j].load(cp - t * D);
+    // Buffer loads: one descriptor per volume over the wave's RPW rows, the
+    // lane's row/disparity offset in a VGPR and the column (x = W1 - 1 - t)
+    // in the scalar offset, so the per-step address update is SALU work.
+    const int ybase = (int)blockIdx.x * RPW;  // <= y
+    const size_t rbase = f * frame + (size_t)ybase * W1 * D;
+    const uint32_t loff = (uint32_t)((y - ybase) * W1 * D + d0);  // elements, even
+    constexpr uint32_t kAccNum = (uint32_t)sizeof(AccT), kAccDen = AccEpu<AccT>::v;  // bytes per element
+    const int nrec_c = RPW * W1 * D * 2;
+    const int nrec_a = (int)((uint32_t)(RPW * W1 * D) * kAccNum / kAccDen);
+    const __amdgpu_buffer_rsrc_t rc_c =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(C + rbase), (short)0, nrec_c, kBufWord3);
+    __amdgpu_buffer_rsrc_t rc_a[NACC];
 #pragma unroll
-        for (int i = 0; i < NACC; i++) AR::load(acc_add(sp, -t * D + (ptrdiff_t)i * (ptrdiff_t)plane), ab[j][i]);
+    for (int i = 0; i < NACC; i++)
+        rc_a[i] = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)acc_add(A, (ptrdiff_t)(rbase + (size_t)i * plane)), (short)0, nrec_a, kBufWord3);
+    const uint32_t vo_c = 2u * loff, vo_a = loff * kAccNum / kAccDen;
+    auto prefetch = [&](int j, ptrdiff_t t) {
+        const uint32_t xd = (uint32_t)((W1 - 1 - (int)t) * D);
+        buf_words<4 * NP>(rc_c, vo_c, 2u * xd, cb[j].v);
+#pragma unroll
+        for (int i = 0; i < NACC; i++)
+            buf_words<2 * NP * kAccNum / kAccDen>(rc_a[i], vo_a, xd * kAccNum / kAccDen, ab[j][i]);
     };
 #pragma unroll
     for (int j = 0; j < PF; j++) prefetch(j, min(j, W1 - 1));
