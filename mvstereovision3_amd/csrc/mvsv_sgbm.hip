@@ -1690,10 +1690,13 @@ __device__ __forceinline__ void sgm_step_seg_t(const uint32_t (&lp)[NP], uint32_
         sgm_step_row_t<NP>(lp, delta2, p1x2, c, ln, t);
     } else {
         const uint32_t MAXP = 0x7fff7fffu;
-        const uint32_t ph = wave_shr1(lp[NP - 1], MAXP);
-        const uint32_t nl = wave_shl1(lp[0], MAXP);
-        const uint32_t prev_hi = seg_first ? MAXP : ph;
-        const uint32_t next_lo = seg_last ? MAXP : nl;
+        // zero-filled wave shifts (bound_ctrl) OR'ed with MAX at the segment
+        // ends (L values are in [0, 0x7fff], so x | MAXP == MAXP): one
+        // v_or_b32_dpp per neighbour
+        const uint32_t prev_hi =
+            (uint32_t)__builtin_amdgcn_mov_dpp((int)lp[NP - 1], 0x138, 0xf, 0xf, true) | (seg_first ? MAXP : 0u);
+        const uint32_t next_lo =
+            (uint32_t)__builtin_amdgcn_mov_dpp((int)lp[0], 0x130, 0xf, 0xf, true) | (seg_last ? MAXP : 0u);
         uint32_t X[NP + 1];  // X[q + 1] = X_q, X[0] = X_{-1}
         X[0] = pk_min(prev_hi, lp[0]);
 #pragma unroll
