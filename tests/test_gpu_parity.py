@@ -97,6 +97,25 @@ def test_sgbm_synthetic_modes(gpu, mvsv, oracle, mode, D):
     assert np.array_equal(got, want), report(got, want)
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_sgbm_wide_disparity_odd_rows(gpu, mvsv, oracle, seed):
+    # D >= 128 runs the 32-lanes-per-row final kernel (two image rows per wave,
+    # buffer-descriptor prefetch): odd heights leave the last wave half-empty
+    rng = np.random.default_rng(7000 + seed)
+    D = 128 if seed < 6 else 256
+    H = int(rng.integers(9, 60)) | 1
+    W = D + int(rng.integers(40, 90))
+    kw = dict(minDisparity=int(rng.integers(-4, 4)), numDisparities=D,
+              blockSize=int(rng.choice([1, 3, 5, 9, 13])),
+              P1=int(rng.choice([0, 8, 72])), P2=int(rng.choice([0, 5, 288, 2000])),
+              disp12MaxDiff=int(rng.integers(-1, 3)), preFilterCap=int(rng.choice([0, 31, 63])),
+              uniquenessRatio=int(rng.choice([0, 5, 15])),
+              speckleWindowSize=int(rng.choice([0, 20])), speckleRange=2, mode=int(rng.integers(0, 2)))
+    L, R = rand_pair(rng, H, W, int(rng.integers(0, 24)), int(rng.integers(0, 3)))
+    got, want = sgbm_both(mvsv, oracle, L, R, **kw)
+    assert np.array_equal(got, want), f"{kw} H={H} W={W}: " + report(got, want)
+
+
 @pytest.mark.parametrize("bs", [13, 15, 17, 21])
 @pytest.mark.parametrize("D", [64, 128])
 def test_sgbm_block_sizes(gpu, mvsv, oracle, bs, D):
