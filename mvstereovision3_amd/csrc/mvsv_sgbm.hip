@@ -675,6 +675,13 @@ __host__ __device__ __forceinline__ T* acc_add(T* p, ptrdiff_t e)
     return p + e / AccEpu<T>::v;  // e is even for nib2_t (d0 and D are even)
 }
 static_assert(AccEpu<const nib2_t>::v == 2 && AccEpu<const uint8_t>::v == 1, "accumulator units");
+// non-negative 32-bit offsets: the unit division is a shift and the 64-bit
+// address add needs no sign extension
+template <typename T>
+__device__ __forceinline__ T* acc_addu(T* p, uint32_t e)
+{
+    return p + e / (uint32_t)AccEpu<T>::v;
+}
 
 __device__ __forceinline__ Line line_geometry(int line, int dx, int dy, int W1, int H)
 {
@@ -1422,8 +1429,8 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     auto cell_x = [&](int t) { return U - (H - 1) + t; };
     const int c0D = ((sy > 0 ? 0 : (H - 1) * W1) + U - (H - 1)) * D;
     const int cstepD = (sy * W1 + 1) * D;
-    auto cell_off = [&](int t) -> int {
-        return (unsigned)cell_x(t) < (unsigned)W1 ? c0D + t * cstepD : 0;
+    auto cell_off = [&](int t) -> uint32_t {  // >= 0: in-image cells only
+        return (unsigned)cell_x(t) < (unsigned)W1 ? (uint32_t)(c0D + t * cstepD) : 0u;
     };
     uint32_t la[NP];
 #pragma unroll
@@ -1484,7 +1491,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
                 // sum of the three deltas t_r + P2, exact in u16 wrap arithmetic
                 o[p] = pk_add_u16(pk_add_u16(ta[p], tb_[p]), pk_add_u16(tc[p], p2x3));
             }
-            AV::store(valid ? acc_add(Af, cell_off(t)) : dp, o);
+            AV::store(valid ? acc_addu(Af, cell_off(t)) : dp, o);
             if (__builtin_expect(!__all(valid), 0)) {
 #pragma unroll
                 for (int p = 0; p < NP; p++) {
