@@ -82,7 +82,17 @@ enum {
     MVSV_E_OOM = -3,         /* device or host allocation failed */
     MVSV_E_IO = -4,          /* cannot open file */
     MVSV_E_PARSE = -5,       /* missing / malformed YAML key */
-    MVSV_E_NODEV = -6        /* no HIP device available */
+    MVSV_E_NODEV = -6,       /* no HIP device available */
+    MVSV_E_TIMEOUT = -7      /* a strip-to-strip hand-off of the SGBM path kernel was
+                                given up: the affected maps are all INVALID */
+};
+
+/* Context options (mvsv_set_option). */
+enum {
+    /* polls a strip-boundary wait of the SGBM path kernel makes before it gives
+     * up (default 1 << 20, ~1 s); 0 gives up at the first poll that finds the
+     * producer's data not yet written (fault injection for tests) */
+    MVSV_OPT_STRIP_SPIN_LIMIT = 1
 };
 
 /* StereoSGBM modes (cv::StereoSGBM::MODE_SGBM / MODE_HH). */
@@ -160,7 +170,12 @@ MVSV_API const char* mvsv_last_error(const mvsv_ctx* ctx);
 MVSV_API int mvsv_set_stream(mvsv_ctx* ctx, void* hip_stream);
 MVSV_API int mvsv_use_own_stream(mvsv_ctx* ctx);
 MVSV_API void* mvsv_get_stream(mvsv_ctx* ctx);
+/* Waits for the context stream; MVSV_E_TIMEOUT if an SGBM launch since the last
+ * check gave up a strip hand-off (its maps were written as all INVALID).  The
+ * device calls also return MVSV_E_TIMEOUT, without enqueueing, when an earlier
+ * launch that has completed by then gave up. */
 MVSV_API int mvsv_synchronize(mvsv_ctx* ctx);
+MVSV_API int mvsv_set_option(mvsv_ctx* ctx, int option, long long value);
 /* Release cached device buffers. */
 MVSV_API int mvsv_trim(mvsv_ctx* ctx);
 

@@ -6,8 +6,9 @@ src/disparity.cpp:6-108).  Compute lives in hand-written HIP kernels for
 gfx950 behind the C ABI of libmvsv.so (include/mvsv.h); this package is the
 host-side mirror of the reference interface.
 """
-from ._lib import (MODE_HH, MODE_SGBM, PREFILTER_NORMALIZED_RESPONSE, PREFILTER_XSOBEL,
-                   VARIANT_FIRSTCOL_FIX, VARIANT_WTA_MIN_D, MvsvError)
+from ._lib import (MODE_HH, MODE_SGBM, MVSV_E_TIMEOUT, OPT_STRIP_SPIN_LIMIT,
+                   PREFILTER_NORMALIZED_RESPONSE, PREFILTER_XSOBEL, VARIANT_FIRSTCOL_FIX,
+                   VARIANT_WTA_MIN_D, MvsvError, set_option, synchronize)
 from .disparity import (Disparity, StereoBM, StereoSGBM, Stereopair, mean_disparity_grid,
                         sgbmParameters, synth_pair)
 from .detection import DisparityStream, MeanDisparityDetection, Subimage, create_dmap_rois
@@ -20,5 +21,6 @@ __all__ = [
     "PREFILTER_NORMALIZED_RESPONSE", "VARIANT_FIRSTCOL_FIX", "VARIANT_WTA_MIN_D",
     "DisparityStream", "MeanDisparityDetection", "Subimage", "create_dmap_rois", "Utility",
     "dMapValues", "ply", "reproject", "init_undistort_rectify_map", "rectify_pair", "remap",
+    "synchronize", "set_option", "MVSV_E_TIMEOUT", "OPT_STRIP_SPIN_LIMIT",
 ]
 __version__ = "1.0.0"

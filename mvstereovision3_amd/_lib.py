@@ -23,6 +23,9 @@ MVSV_E_OOM = -3
 MVSV_E_IO = -4
 MVSV_E_PARSE = -5
 MVSV_E_NODEV = -6
+MVSV_E_TIMEOUT = -7
+
+OPT_STRIP_SPIN_LIMIT = 1
 
 MODE_SGBM = 0
 MODE_HH = 1
@@ -40,6 +43,7 @@ _CODES = {
     MVSV_E_IO: "cannot open file",
     MVSV_E_PARSE: "missing or malformed key",
     MVSV_E_NODEV: "no HIP device",
+    MVSV_E_TIMEOUT: "strip hand-off gave up",
 }
 
 
@@ -107,6 +111,7 @@ def _declare(lib, strict=True):
         "mvsv_use_own_stream": ([P], I),
         "mvsv_get_stream": ([P], P),
         "mvsv_synchronize": ([P], I),
+        "mvsv_set_option": ([P, I, ctypes.c_longlong], I),
         "mvsv_trim": ([P], I),
         "mvsv_sgbm": ([P, P, Z, P, Z, I, I, P, P, Z], I),
         "mvsv_bm": ([P, P, Z, P, Z, I, I, P, P, Z], I),
@@ -209,6 +214,20 @@ def context(device: int = 0) -> Context:
     if c is None:
         c = ctxs[device] = Context(device)
     return c
+
+
+def synchronize(device: int = 0) -> None:
+    """Wait for the device work of this thread's context on `device` and raise
+    MvsvError(MVSV_E_TIMEOUT) if an SGBM launch since the last check gave up a
+    strip hand-off (its maps were written as all INVALID).  Call it where a
+    torch.cuda.synchronize() would make the maps visible to the host."""
+    c = context(device)
+    check(lib().mvsv_synchronize(c.handle), c.handle)
+
+
+def set_option(option: int, value: int, device: int = 0) -> None:
+    c = context(device)
+    check(lib().mvsv_set_option(c.handle, int(option), int(value)), c.handle)
 
 
 def profile_enable(ctx: Context, on: bool = True):

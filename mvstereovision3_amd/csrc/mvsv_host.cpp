@@ -52,6 +52,39 @@ int ensure(mvsv_ctx* ctx, DevBuf& b, size_t bytes, const char* what)
     return MVSV_OK;
 }
 
+int check_report(mvsv_ctx* ctx)
+{
+    if (!ctx->report) return MVSV_OK;
+    const int v = __atomic_load_n(ctx->report, __ATOMIC_ACQUIRE);
+    if (v == 0) return MVSV_OK;
+    __atomic_store_n(ctx->report, 0, __ATOMIC_RELEASE);
+    return set_error(ctx, MVSV_E_TIMEOUT,
+                     "sgbm path kernel: a strip-boundary wait gave up (that launch's maps are all "
+                     "INVALID)");
+}
+
+int alloc_report(mvsv_ctx* ctx, int count, int** host, int** dev)
+{
+    *host = nullptr;
+    *dev = nullptr;
+    void* h = nullptr;
+    // fine-grained, coherent: kernels store into it with system scope and the
+    // host reads it without a copy
+    hipError_t e = hipHostMalloc(&h, sizeof(int) * (size_t)count,
+                                 hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return check_hip(ctx, e, "report word allocation");
+    std::memset(h, 0, sizeof(int) * (size_t)count);
+    void* d = nullptr;
+    e = hipHostGetDevicePointer(&d, h, 0);
+    if (e != hipSuccess) {
+        (void)hipHostFree(h);
+        return check_hip(ctx, e, "report word mapping");
+    }
+    *host = (int*)h;
+    *dev = (int*)d;
+    return MVSV_OK;
+}
+
 static hipEvent_t pool_get(mvsv_ctx* ctx)
 {
     if (!ctx->event_pool.empty()) {
@@ -250,13 +283,20 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
     mvsv_ctx* c = new (std::nothrow) mvsv_ctx();
     if (!c) return MVSV_E_OOM;
     c->device = hip_device;
-    if (hipSetDevice(hip_device) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    DeviceGuard dev_guard(hip_device);
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_switch, hipEventDisableTiming) != hipSuccess ||
+        alloc_report(c, 1, &c->report, &c->report_dev) != MVSV_OK) {
         (void)hipGetLastError();
+        if (c->ev_switch) (void)hipEventDestroy(c->ev_switch);
+        if (c->own) (void)hipStreamDestroy(c->own);
         delete c;
         return MVSV_E_HIP;
     }
+    c->report_target = c->report_dev;
     c->stream = c->own;
+    if (const char* v = std::getenv("MVSV_STRIP_SPIN_LIMIT"))
+        c->spin_limit = (unsigned)std::strtoul(v, nullptr, 0);
     // kernel-variant switches for A/B measurement and for testing the
     // general-shape kernels on shapes the specialised ones also cover
     if (const char* v = std::getenv("MVSV_KERNELS")) {
@@ -280,7 +320,7 @@ static void free_buf(DevBuf& b)
 int mvsv_trim(mvsv_ctx* ctx)
 {
     if (!ctx) return MVSV_E_INVALID_ARG;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     DevBuf* all[] = {&ctx->pre, &ctx->cost, &ctx->agg, &ctx->raw, &ctx->uf_parent, &ctx->uf_size,
                      &ctx->uf_tile, &ctx->tri_bnd, &ctx->status,
@@ -322,7 +362,7 @@ int mvsv_profile_reset(mvsv_ctx* ctx)
 int mvsv_profile_read(mvsv_ctx* ctx, double* ms, int* launches, int n)
 {
     if (!ctx || n < 0) return MVSV_E_INVALID_ARG;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     int rc = check_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
     if (rc) return rc;
     for (int i = 0; i < n; i++) {
@@ -350,6 +390,8 @@ void mvsv_destroy(mvsv_ctx* ctx)
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->ev_switch) (void)hipEventDestroy(ctx->ev_switch);
+    if (ctx->report) (void)hipHostFree(ctx->report);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
     delete ctx;
@@ -357,42 +399,55 @@ void mvsv_destroy(mvsv_ctx* ctx)
 
 const char* mvsv_last_error(const mvsv_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+// Every launch of a context shares its cached buffers, so work enqueued on a
+// new stream must not start before the work already on the previous one: the
+// new stream waits on an event recorded on the old (no host synchronisation).
+static int switch_stream(mvsv_ctx* ctx, hipStream_t s)
+{
+    if (s == ctx->stream) return MVSV_OK;
+    DeviceGuard dev_guard(ctx->device);
+    int rc;
+    if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_switch, ctx->stream), "stream switch record")) ||
+        (rc = check_hip(ctx, hipStreamWaitEvent(s, ctx->ev_switch, 0), "stream switch wait")))
+        return rc;
+    ctx->stream = s;
+    return MVSV_OK;
+}
+
 int mvsv_set_stream(mvsv_ctx* ctx, void* s)
 {
     if (!ctx) return MVSV_E_INVALID_ARG;
-    ctx->stream = (hipStream_t)s;  // NULL = the HIP null stream
-    return MVSV_OK;
+    return switch_stream(ctx, (hipStream_t)s);  // NULL = the HIP null stream
 }
 
 int mvsv_use_own_stream(mvsv_ctx* ctx)
 {
     if (!ctx) return MVSV_E_INVALID_ARG;
-    ctx->stream = ctx->own;
-    return MVSV_OK;
+    return switch_stream(ctx, ctx->own);
+}
+
+int mvsv_set_option(mvsv_ctx* ctx, int option, long long value)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    switch (option) {
+    case MVSV_OPT_STRIP_SPIN_LIMIT:
+        if (value < 0 || value > 0xffffffffLL)
+            return set_error(ctx, MVSV_E_INVALID_ARG, "spin limit must be 0..2^32-1");
+        ctx->spin_limit = (unsigned)value;
+        return MVSV_OK;
+    default:
+        return set_error(ctx, MVSV_E_INVALID_ARG, "unknown option");
+    }
 }
 
 void* mvsv_get_stream(mvsv_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
-// Device status word (set by a kernel that had to give up, e.g. a strip-boundary
-// wait of the sheared-strip path kernel that timed out): read after a sync.
-static int check_status(mvsv_ctx* ctx)
-{
-    if (!ctx->status.ptr) return MVSV_OK;
-    int v = 0;
-    int rc = check_hip(ctx, hipMemcpy(&v, ctx->status.ptr, sizeof(v), hipMemcpyDeviceToHost),
-                       "status read");
-    if (rc) return rc;
-    if (v == 0) return MVSV_OK;
-    (void)hipMemset(ctx->status.ptr, 0, sizeof(v));
-    return set_error(ctx, MVSV_E_HIP, "sgbm path kernel: strip-boundary wait timed out");
-}
-
 int mvsv_synchronize(mvsv_ctx* ctx)
 {
     if (!ctx) return MVSV_E_INVALID_ARG;
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     int rc = check_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
-    return rc ? rc : check_status(ctx);
+    return rc ? rc : check_report(ctx);
 }
 
 size_t mvsv_sgbm_workspace_bytes(int n, int W, int H, const mvsv_sgbm_params* p)
@@ -419,7 +474,10 @@ int mvsv_sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t l
     std::string why;
     int rc = resolve_sgbm(p, W, H, &e, &why);
     if (rc) return set_error(ctx, rc, why);
-    (void)hipSetDevice(ctx->device);
+    // an earlier launch that has finished by now gave up a strip wait: its
+    // maps are INVALID; say so before anything else runs on this context
+    if ((rc = check_report(ctx))) return rc;
+    DeviceGuard dev_guard(ctx->device);
     return sgbm_device(ctx, n, L, ls, lfs, R, rs, rfs, W, H, e, out, os, ofs);
 }
 
@@ -435,7 +493,7 @@ int mvsv_bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs
     std::string why;
     int rc = resolve_bm(p, W, H, &e, &why);
     if (rc) return set_error(ctx, rc, why);
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     return bm_device(ctx, n, L, ls, lfs, R, rs, rfs, W, H, e, out, os, ofs);
 }
 
@@ -445,7 +503,7 @@ int mvsv_mean_disparity_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap, s
     if (!ctx) return MVSV_E_INVALID_ARG;
     if (n <= 0 || !dmap || !means || W <= 0 || H <= 0 || st < (size_t)W)
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad mean-grid arguments");
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     return mean_grid_device(ctx, n, dmap, st, fs, W, H, means);
 }
 
@@ -465,7 +523,8 @@ static int host_call(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* 
     rc = sgbm ? resolve_sgbm((const mvsv_sgbm_params*)params, W, H, &se, &why)
               : resolve_bm((const mvsv_bm_params*)params, W, H, &be, &why);
     if (rc) return set_error(ctx, rc, why);
-    (void)hipSetDevice(ctx->device);
+    if (sgbm && (rc = check_report(ctx))) return rc;  // an earlier device call's give-up
+    DeviceGuard dev_guard(ctx->device);
     size_t fb = (size_t)W * H;
     if ((rc = ensure(ctx, ctx->h_left, fb, "left staging"))) return rc;
     if ((rc = ensure(ctx, ctx->h_right, fb, "right staging"))) return rc;
@@ -481,7 +540,7 @@ static int host_call(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* 
     if (rc) return rc;
     if ((rc = check_hip(ctx, hipMemcpy2DAsync(out, os * 2, dout, (size_t)W * 2, (size_t)W * 2, H, hipMemcpyDeviceToHost, s), "D2H out"))) return rc;
     if ((rc = check_hip(ctx, hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
-    return check_status(ctx);
+    return check_report(ctx);
 }
 
 int mvsv_sgbm(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* R, size_t rs, int W,
@@ -662,7 +721,7 @@ int mvsv_reproject_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, 
     if (!ctx) return MVSV_E_INVALID_ARG;
     if (n <= 0 || !dmap || !Q || !xyzw || W <= 0 || H <= 0 || st < (size_t)W || xs < (size_t)W)
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad reprojection arguments");
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     return reproject_device(ctx, n, dmap, st, fs, W, H, Q, xyzw, xs, xfs);
 }
 
@@ -766,7 +825,7 @@ int mvsv_dmap2pcl(mvsv_ctx* ctx, const char* path, const int16_t* dmap, size_t s
     if (!ctx) return MVSV_E_INVALID_ARG;
     if (!path || !dmap || !Q || W <= 0 || H <= 0 || st < (size_t)W)
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad dmap2pcl arguments");
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     const size_t px = (size_t)W * H;
     int rc;
     if ((rc = ensure(ctx, ctx->h_out, px * 2, "dmap staging"))) return rc;
@@ -808,7 +867,7 @@ int mvsv_remap_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_
     if (n <= 0 || !src || !mx || !my || !dst || sw <= 0 || sh <= 0 || dw <= 0 || dh <= 0 ||
         ss < (size_t)sw || ds < (size_t)dw || ms < (size_t)dw)
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad remap arguments");
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     return remap_device(ctx, n, src, ss, sfs, sw, sh, mx, my, ms, dst, ds, dfs, dw, dh);
 }
 
@@ -825,7 +884,7 @@ int mvsv_rectify_pair(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t*
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad rectification arguments");
     for (int i = 0; i < 4; i++)
         if (!maps[i]) return set_error(ctx, MVSV_E_INVALID_ARG, "null map");
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     const size_t px = (size_t)W * H;
     int rc;
     if ((rc = ensure(ctx, ctx->h_left, 2 * px, "rectify staging")) ||

@@ -52,6 +52,35 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+// Entry points switch to the context's device and give the caller's current
+// device back on return (a compute on cuda:1 must not change the thread's
+// device under the torch code that runs next).
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) {
+            (void)hipGetLastError();
+            prev = -1;
+        }
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
+// Default number of polls a strip-boundary wait of the sheared-strip kernel
+// makes before it gives up (each poll = one s_sleep + one L2 load of the
+// producer's granule, ~1 us): ~1 s, far beyond any producer delay of a
+// healthy launch; the wait only exists to turn a lost hand-off into an error
+// instead of a hang.  mvsv_set_option(MVSV_OPT_STRIP_SPIN_LIMIT) overrides it.
+constexpr unsigned kStripSpinLimitDefault = 1u << 20;
+
 }  // namespace mvsv
 
 struct mvsv_ctx {
@@ -61,7 +90,19 @@ struct mvsv_ctx {
     std::string err;
     // SGBM
     mvsv::DevBuf pre, cost, agg, raw, uf_parent, uf_size, uf_tile, dummy, keys, tri_bnd, status;
-    unsigned tri_epoch = 0;  // tag of the strip-boundary granules of the last launch
+    // launch number of the last sheared-strip launch: its low 16 bits tag the
+    // boundary granules (tri_bnd is re-zeroed whenever they wrap), all 32 bits
+    // go into status[0] when that launch gives up a wait (no per-call reset)
+    unsigned tri_epoch = 0;
+    unsigned spin_limit = mvsv::kStripSpinLimitDefault;
+    // given-up strip waits are reported into host-mapped ints: `report` is the
+    // context's sticky word (device calls; read and cleared by the next call,
+    // mvsv_synchronize and the host-pointer calls), report_target is where the
+    // next launches report (a frame stream points it at its run's own word)
+    int* report = nullptr;      // host view
+    int* report_dev = nullptr;  // device view of report
+    int* report_target = nullptr;
+    hipEvent_t ev_switch = nullptr;  // orders a new stream after the previous one
     hipStream_t aux = nullptr;  // second stream for concurrent direction passes
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int path16 = 1;  // 16-lanes-per-scanline path kernels where D allows
@@ -88,6 +129,11 @@ namespace mvsv {
 int set_error(mvsv_ctx* ctx, int code, const std::string& msg);
 int ensure(mvsv_ctx* ctx, DevBuf& b, size_t bytes, const char* what);
 int check_hip(mvsv_ctx* ctx, hipError_t e, const char* what);
+// Reads and clears the context's sticky report word: MVSV_E_TIMEOUT if a
+// strip-boundary wait of an earlier launch gave up.  No synchronisation.
+int check_report(mvsv_ctx* ctx);
+// Host-mapped int (host and device views), zeroed.
+int alloc_report(mvsv_ctx* ctx, int count, int** host, int** dev);
 
 enum Stage {
     kStagePre = 0,
@@ -120,8 +166,12 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
               size_t rs, size_t rfs, int W, int H, const BmEff& e, int16_t* out, size_t os,
               size_t ofs);
 // Post filters shared by both matchers.
+// poison != nullptr: when *poison == epoch (the launch `epoch` gave up a strip
+// wait) every output pixel is `invalid` instead of the median -- no map computed
+// from stale hand-off data leaves the pipeline.
 int median3x3_device(mvsv_ctx* ctx, int n, const int16_t* src, size_t ss, size_t sfs,
-                     int16_t* dst, size_t ds, size_t dfs, int W, int H);
+                     int16_t* dst, size_t ds, size_t dfs, int W, int H,
+                     const int* poison = nullptr, unsigned epoch = 0, int invalid = 0);
 int speckle_device(mvsv_ctx* ctx, int n, int16_t* img, size_t st, size_t fs, int W, int H,
                    int new_val, int max_size, int max_diff);
 int remap_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_t sfs, int sw, int sh,

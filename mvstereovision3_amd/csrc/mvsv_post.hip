@@ -39,12 +39,18 @@ __device__ __forceinline__ int med9(int p0, int p1, int p2, int p3, int p4, int 
 
 __global__ __launch_bounds__(256) void median3x3_kernel(const int16_t* __restrict__ src, size_t ss,
                                                         size_t sfs, int16_t* __restrict__ dst,
-                                                        size_t ds, size_t dfs, int W, int H)
+                                                        size_t ds, size_t dfs, int W, int H,
+                                                        const int* __restrict__ poison,
+                                                        unsigned epoch, int invalid)
 {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
     const int f = blockIdx.z;
     if (x >= W || y >= H) return;
+    if (poison && __builtin_expect(*poison == (int)epoch, 0)) {
+        dst[f * dfs + (size_t)y * ds + x] = (int16_t)invalid;
+        return;
+    }
     const int16_t* s = src + f * sfs;
     const int xm = max(x - 1, 0), xp = min(x + 1, W - 1);
     const int16_t* r0 = s + (size_t)max(y - 1, 0) * ss;
@@ -434,11 +440,12 @@ __global__ __launch_bounds__(256) void reproject_kernel(const int16_t* __restric
 }  // namespace
 
 int median3x3_device(mvsv_ctx* ctx, int n, const int16_t* src, size_t ss, size_t sfs, int16_t* dst,
-                     size_t ds, size_t dfs, int W, int H)
+                     size_t ds, size_t dfs, int W, int H, const int* poison, unsigned epoch,
+                     int invalid)
 {
     dim3 grid((W + 63) / 64, (H + 3) / 4, n);
     hipLaunchKernelGGL(median3x3_kernel, grid, dim3(256), 0, ctx->stream, src, ss, sfs, dst, ds,
-                       dfs, W, H);
+                       dfs, W, H, poison, epoch, invalid);
     return check_hip(ctx, hipGetLastError(), "median3x3");
 }
 

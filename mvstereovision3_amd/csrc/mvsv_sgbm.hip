@@ -1220,7 +1220,6 @@ struct TriCfg {
 constexpr int kTriPF = 2;               // steps of C prefetch (compute waves)
 constexpr int kTriBF = 4;               // steps of boundary prefetch (comm wave)
 constexpr int kTriUnroll = 4;           // lcm(kTriPF, kTriBF, 2)
-constexpr unsigned kTriSpinLimit = 1u << 16;
 
 template <int NP>
 struct TriLayout {
@@ -1285,8 +1284,8 @@ __global__ __launch_bounds__(TriCfg<NP>::kThreads)
 __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     const int16_t* __restrict__ C, AccT* __restrict__ A, size_t plane, AccT* __restrict__ dummy,
     int H, int W1, int D, int npass, int P1, int P2, unsigned long long* __restrict__ bnd,
-    unsigned epoch, int nframes, int nstrips, int* __restrict__ status,
-    unsigned long long* __restrict__ stats)
+    unsigned epoch, int nframes, int nstrips, int* __restrict__ status, unsigned spin_limit,
+    int* __restrict__ report, unsigned long long* __restrict__ stats)
 {
     using AV = AccVec<NP, AccT>;
     using TL = TriLayout<NP>;
@@ -1375,13 +1374,19 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
             const unsigned long long sp0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
             unsigned spins = 0;
             while (!__all(ok)) {
-                // give up after kTriSpinLimit polls, or at once when any block gave up
-                if (++spins > kTriSpinLimit) {
-                    if (lane == 0) atomicOr(status, 1);
+                // give up after spin_limit polls, or soon after any block of
+                // this launch gave up (status = this launch's epoch): the
+                // launch then drains, the median kernel writes its maps as
+                // INVALID and the host reports MVSV_E_TIMEOUT
+                if (++spins > spin_limit) {
+                    if (lane == 0) {
+                        __hip_atomic_store(status, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(report, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                     break;
                 }
                 if ((spins & 63) == 0 &&
-                    __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+                    __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)epoch)
                     break;
                 __builtin_amdgcn_s_sleep(1);
                 const unsigned long long* q = bsrc + (size_t)clampi(t, 0, H - 1) * bstep;
@@ -2228,7 +2233,15 @@ int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT*
         if ((rc = check_hip(ctx, hipMemsetAsync(ctx->status.ptr, 0, 16, ctx->stream), "status reset")))
             return rc;
     }
-    if ((++ctx->tri_epoch & 0xffffu) == 0) ++ctx->tri_epoch;  // tag 0 = never written
+    // Launch epochs never repeat between two zeroings of the granules: tag 0
+    // means "never written", and when the 16-bit tag wraps every slot is
+    // zeroed again, so a slot carrying this launch's tag was written by it.
+    if ((++ctx->tri_epoch & 0xffffu) == 0) {
+        ++ctx->tri_epoch;
+        if ((rc = check_hip(ctx, hipMemsetAsync(ctx->tri_bnd.ptr, 0, ctx->tri_bnd.bytes, ctx->stream),
+                            "sgbm boundary reset")))
+            return rc;
+    }
     const unsigned epoch = ctx->tri_epoch;
     dim3 grid(nstrips * npass * n);
     unsigned long long* stats = nullptr;
@@ -2240,7 +2253,7 @@ int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT*
     hipLaunchKernelGGL((sgbm_tri_kernel<NP, AccT>), grid, dim3(TriCfg<NP>::kThreads), TL::kBytes,
                        ctx->stream, Cv, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, npass, e.P1,
                        e.P2, (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips,
-                       (int*)ctx->status.ptr, stats);
+                       (int*)ctx->status.ptr, ctx->spin_limit, ctx->report_target, stats);
     rc = check_hip(ctx, hipGetLastError(), "sgbm sheared-strip path kernel");
     if (want_stats) {
         (void)hipStreamSynchronize(ctx->stream);
@@ -2522,6 +2535,7 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     int16_t* Cv = (int16_t*)ctx->cost.ptr;
     void* Sv = ctx->agg.ptr;
     int16_t* raw = (int16_t*)ctx->raw.ptr;
+    const unsigned epoch0 = ctx->tri_epoch;
 
     {
         StageTimer tm(ctx, kStagePre);
@@ -2569,8 +2583,13 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     else rc = launch_paths_acc<4>(ctx, n, H, W, e, Cv, Sv, raw);
     if (rc) return rc;
 
+    // a strip launch of this call that gave up a wait poisons the median's output
+    const bool strips_ran = ctx->tri_epoch != epoch0;
     StageTimer tm(ctx, kStagePost);
-    if ((rc = median3x3_device(ctx, n, raw, W, plane, out, os, ofs, W, H))) return rc;
+    if ((rc = median3x3_device(ctx, n, raw, W, plane, out, os, ofs, W, H,
+                               strips_ran ? (const int*)ctx->status.ptr : nullptr, ctx->tri_epoch,
+                               e.invalid)))
+        return rc;
     if (e.speckle_window > 0)
         return speckle_device(ctx, n, out, os, ofs, W, H, e.invalid, e.speckle_window,
                               e.speckle_diff);

@@ -38,11 +38,17 @@ struct mvsv_stream {
         float* dMeans = nullptr;
         hipEvent_t uploaded = nullptr, computed = nullptr, done = nullptr;
         int status = MVSV_OK;
+        int run_len = 0;     // > 0: this slot starts a frame-batch launch of run_len slots
+        bool gave_up = false;  // the launch of this frame gave up a strip wait
     };
     std::vector<Slot> slots;
     uint8_t *dL_all = nullptr, *dR_all = nullptr;  // [depth][H][W]
     int16_t* dOut_all = nullptr;
     float* dMeans_all = nullptr;  // [depth][81]
+    // per-slot report words (host-mapped): a launch starting at slot i reports
+    // a given-up strip wait into rep[i], read when slot i is popped
+    int* rep = nullptr;
+    int* rep_dev = nullptr;
     long head = 0, tail = 0;      // pushed / popped frame counters
     long launched = 0;            // frames whose compute is enqueued
     int batch = 1;
@@ -62,6 +68,7 @@ static void stream_free(mvsv_stream* st)
     if (st->dR_all) (void)hipFree(st->dR_all);
     if (st->dOut_all) (void)hipFree(st->dOut_all);
     if (st->dMeans_all) (void)hipFree(st->dMeans_all);
+    if (st->rep) (void)hipHostFree(st->rep);
     if (st->up) (void)hipStreamDestroy(st->up);
     if (st->down) (void)hipStreamDestroy(st->down);
     delete st;
@@ -80,7 +87,7 @@ int mvsv_stream_create(mvsv_ctx* ctx, int W, int H, const mvsv_sgbm_params* p, i
     if (grid_roi && (grid_roi->x0 < 0 || grid_roi->y0 < 0 || grid_roi->x1 > W || grid_roi->y1 > H ||
                      grid_roi->x1 - grid_roi->x0 < 9 || grid_roi->y1 - grid_roi->y0 < 9))
         return set_error(ctx, MVSV_E_INVALID_ARG, "grid ROI outside the image or smaller than 9x9");
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     mvsv_stream* st = new (std::nothrow) mvsv_stream();
     if (!st) return MVSV_E_OOM;
     st->ctx = ctx;
@@ -113,6 +120,7 @@ int mvsv_stream_create(mvsv_ctx* ctx, int W, int H, const mvsv_sgbm_params* p, i
              hipEventCreateWithFlags(&s.computed, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
     }
+    ok = ok && alloc_report(ctx, depth, &st->rep, &st->rep_dev) == MVSV_OK;
     if (!ok) {
         (void)hipGetLastError();
         stream_free(st);
@@ -139,7 +147,13 @@ static int stream_launch(mvsv_stream* st)
         // the upload stream is in order: the last slot's upload covers the run
         if ((rc = check_hip(ctx, hipStreamWaitEvent(ctx->stream, last.uploaded, 0), "stream wait")))
             return rc;
+        // slot i0 was popped (or never used): nothing reads rep[i0] any more
+        __atomic_store_n(&st->rep[i0], 0, __ATOMIC_RELEASE);
+        first.run_len = n;
+        int* prev_target = ctx->report_target;
+        ctx->report_target = st->rep_dev + i0;
         int status = sgbm_device(ctx, n, first.dL, W, px, first.dR, W, px, W, H, st->eff, first.dOut, W, px);
+        ctx->report_target = prev_target;
         if (status == MVSV_OK && st->grid) {
             const mvsv_rect& q = st->roi;
             status = mean_grid_device(ctx, n, first.dOut + (size_t)q.y0 * W + q.x0, W, px, q.x1 - q.x0,
@@ -170,7 +184,7 @@ int mvsv_stream_set_batch(mvsv_stream* st, int batch)
     if (!st) return MVSV_E_INVALID_ARG;
     if (batch < 1 || batch > (int)st->slots.size())
         return set_error(st->ctx, MVSV_E_INVALID_ARG, "stream batch must be 1..depth");
-    (void)hipSetDevice(st->ctx->device);
+    DeviceGuard dev_guard(st->ctx->device);
     int rc = stream_launch(st);  // frames already pushed keep the old grouping
     if (rc) return rc;
     st->batch = batch;
@@ -184,7 +198,7 @@ int mvsv_stream_set_params(mvsv_stream* st, const mvsv_sgbm_params* p)
     std::string why;
     int rc = resolve_sgbm(p, st->W, st->H, &e, &why);
     if (rc) return set_error(st->ctx, rc, why);
-    (void)hipSetDevice(st->ctx->device);
+    DeviceGuard dev_guard(st->ctx->device);
     if ((rc = stream_launch(st))) return rc;  // pending frames keep the old parameters
     st->params = *p;  // applies to frames pushed from now on (trgt/mean_test.cpp:348 setters)
     st->eff = e;
@@ -201,7 +215,7 @@ int mvsv_stream_push(mvsv_stream* st, const uint8_t* L, size_t ls, const uint8_t
         return set_error(ctx, MVSV_E_INVALID_ARG, "null frame or stride smaller than width");
     if (st->head - st->tail >= (long)st->slots.size())
         return set_error(ctx, MVSV_E_INVALID_ARG, "stream full: pop a frame first");
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     auto& s = st->slots[st->head % st->slots.size()];
     const int W = st->W, H = st->H;
     // the slot's previous frame was popped, so its copies are complete
@@ -229,13 +243,24 @@ int mvsv_stream_pop(mvsv_stream* st, int16_t* out, size_t os, float* means)
     if (st->head == st->tail) return set_error(ctx, MVSV_E_INVALID_ARG, "stream empty");
     if (out && os < (size_t)st->W) return set_error(ctx, MVSV_E_INVALID_ARG, "stride smaller than width");
     auto& s = st->slots[st->tail % st->slots.size()];
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     int rc = MVSV_OK;
     if (st->tail >= st->launched && (rc = stream_launch(st))) return rc;  // partial group
     rc = check_hip(ctx, hipEventSynchronize(s.done), "stream sync");
+    const long idx = st->tail % (long)st->slots.size();
     st->tail++;
     if (rc) return rc;
+    if (s.run_len > 0) {  // first frame of its launch: that launch has completed
+        const bool gave_up = __atomic_load_n(&st->rep[idx], __ATOMIC_ACQUIRE) != 0;
+        for (int k = 0; k < s.run_len; k++) st->slots[idx + k].gave_up = gave_up;
+        s.run_len = 0;
+    }
     if (s.status) return s.status;
+    if (s.gave_up) {
+        s.gave_up = false;
+        return set_error(ctx, MVSV_E_TIMEOUT,
+                         "stream frame: a strip-boundary wait of its SGBM launch gave up");
+    }
     if (out)
         for (int y = 0; y < st->H; y++)
             std::memcpy(out + (size_t)y * os, s.hOut + (size_t)y * st->W, (size_t)st->W * 2);
@@ -251,7 +276,7 @@ int mvsv_stream_pop(mvsv_stream* st, int16_t* out, size_t os, float* means)
 void mvsv_stream_destroy(mvsv_stream* st)
 {
     if (!st) return;
-    (void)hipSetDevice(st->ctx->device);
+    DeviceGuard dev_guard(st->ctx->device);
     (void)hipStreamSynchronize(st->up);
     (void)hipStreamSynchronize(st->ctx->stream);
     (void)hipStreamSynchronize(st->down);
@@ -264,7 +289,7 @@ int mvsv_mean_disparity_grid(mvsv_ctx* ctx, const int16_t* dmap, size_t st, int 
     if (!ctx) return MVSV_E_INVALID_ARG;
     if (!dmap || !means || W <= 0 || H <= 0 || st < (size_t)W)
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad mean-grid arguments");
-    (void)hipSetDevice(ctx->device);
+    DeviceGuard dev_guard(ctx->device);
     const size_t px = (size_t)W * H;
     int rc;
     if ((rc = ensure(ctx, ctx->h_out, px * 2 + 4 + 81 * sizeof(float), "grid staging"))) return rc;
