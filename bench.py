@@ -15,14 +15,23 @@ median, speckle) with inputs already resident in HBM, plus -- for N > 1 -- the
 RCCL gather of the int16 maps to rank 0 (the only exchange step of the
 frame-parallel batch mode).
 
-Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch with
-python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ...
+Run: python bench.py [--gpus N --steps K --warmup W].  With N > 1 and no
+WORLD_SIZE in the environment, bench.py starts the N ranks itself (a child
+`python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1`,
+before any GPU call) and exits with its status; under an external launcher it
+checks that WORLD_SIZE == N.  --dry rehearses the launcher and the gather on
+CPU (gloo, a trivial host compute, no GPU and no oracle).
 """
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import threading
 import time
@@ -34,10 +43,22 @@ if ROOT not in sys.path:
 SEED0 = 0x5EED0000
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SGBM_YML = os.path.join(ROOT, "tests", "golden", "configs", "sgbm.yml")
-PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+KERNEL_SOURCES = os.path.join(ROOT, "mvstereovision3_amd", "csrc")
+CPU_SHARE = 16  # host cores of one GPU's share on the GPU box
+
+# what bounds each stage (measured); HBM is the roofline quoted
+# because MFMA is unused (integer min/add work, no dense contraction)
+LIMITER = {
+    "path_strips": "VALU issue + strip-chain critical path (three recurrences per byte of C)",
+    "cost_volume": "latency (VALU ~37 %, LDS ~40 % busy)",
+    "final_wta_lr": "VALU issue",
+    "path_lines": "HBM",
+    "post_filters": "launch / atomics",
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -46,15 +67,42 @@ def parse():
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=960)
     ap.add_argument("--mode", type=int, default=1, help="1 = MODE_HH (8 paths), 0 = 5 paths")
-    ap.add_argument("--cpu-frames", type=int, default=8)
-    ap.add_argument("--cpu-threads", type=int, default=8)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0 = the GPU's host-core share, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--dry", action="store_true",
+                    help="CPU rehearsal of launcher + gather (gloo, trivial compute)")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int:
+    """Start args.gpus ranks of this script under torch.distributed.run (a child
+    process; nothing here has touched the GPU) and return its exit status."""
+    if not args.dry:
+        import torch
+        have = torch.cuda.device_count()  # does not initialise the GPU on this image
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {have} GPUs visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True):
-    """Algorithmic HBM bytes of one step per stage ("Kernels").
+    """Implementation HBM bytes of one step per stage ("Kernels").
 
     acc = bytes per (pixel, disparity) of a path-delta accumulator plane (0.5 for
     the 4-bit planes of the strip schedule when 3 * P2 <= 15, 1 when
@@ -62,8 +110,6 @@ def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True):
     {32, 64, 128, 256}): the strip kernel runs npass passes (down, + up for 8
     paths) that each read C and write their own plane, the L->R line kernel
     reads C and writes a plane, the final kernel reads C and every plane.
-    Otherwise one kernel per direction: the first writes the accumulator, the
-    others read and rewrite it, the final kernel reads C and it.
     """
     cells = W1 * H * D
     px = W * H
@@ -88,6 +134,30 @@ def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True):
         "final_wta_lr": final_b,
         "post_filters": F * 4 * px,
     }.get(stage, 0)
+
+
+def kernel_source_sha() -> str:
+    h = hashlib.sha256()
+    for p in sorted(glob.glob(os.path.join(KERNEL_SOURCES, "*.hip")) +
+                    glob.glob(os.path.join(KERNEL_SOURCES, "*.hpp"))):
+        h.update(open(p, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def cpu_info():
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = os.cpu_count() or 1
+    return {"nproc": os.cpu_count(), "affinity": aff, "model": model}
 
 
 def cpu_baseline(frames, params, threads):
@@ -118,8 +188,62 @@ def cpu_baseline(frames, params, threads):
     return time.perf_counter() - t0, outs
 
 
-def main():
-    args = parse()
+def dry_main(args, world, rank):
+    """Launcher + gather rehearsal: gloo ranks, host frames, out = L - R (int16)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import mvstereovision3_amd as mvsv
+    from mvstereovision3_amd.batch import FrameBatch, frame_seeds
+    if world > 1:
+        dist.init_process_group("gloo")
+    W, H, F = args.width, args.height, args.frames
+    seeds = frame_seeds(rank, world, F, SEED0)
+    pairs = [mvsv.synth_pair(sd, W, H, 0, 16) for sd in seeds]
+    L = torch.from_numpy(np.stack([p[0] for p in pairs]))
+    R = torch.from_numpy(np.stack([p[1] for p in pairs]))
+    out = torch.empty((F, H, W), dtype=torch.int16)
+
+    def compute(Lb, Rb, o):
+        o.copy_(Lb.to(torch.int16) - Rb.to(torch.int16))
+
+    batch = FrameBatch(L, R, out, compute, rank, world, gather=world > 1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        got = batch.step()
+    elapsed = time.perf_counter() - t0
+    if rank == 0:
+        got = torch.cat(got) if world > 1 else out
+        ok = 0
+        for r in range(world):
+            for j, sd in enumerate(frame_seeds(r, world, F, SEED0)):
+                Lh, Rh = mvsv.synth_pair(sd, W, H, 0, 16)
+                ok += int(np.array_equal(got[r * F + j].numpy(),
+                                         Lh.astype(np.int16) - Rh.astype(np.int16)))
+        print(json.dumps({"dry": True, "n_gpus": world, "global_batch": F * world,
+                          "gather": "gloo" if world > 1 else "none",
+                          "gathered_frames_ok": f"{ok}/{F * world}",
+                          "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 3)}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def main(argv=None):
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        return 2
+    if args.dry:
+        return dry_main(args, world, rank)
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -127,11 +251,6 @@ def main():
     import mvstereovision3_amd as mvsv
     from mvstereovision3_amd import _lib
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -160,9 +279,6 @@ def main():
     gather = world > 1 and not args.no_gather
     batch = FrameBatch(Lt, Rt, out, lambda L, R, o: m.compute(L, R, o), rank, world, gather)
 
-    def step():
-        batch.step()
-
     def barrier():
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -170,26 +286,32 @@ def main():
         torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
-        step()
+        batch.step()
     ctx = _lib.context(local)
     barrier()
+    _lib.synchronize(local)  # raises if a warm-up launch gave up a strip hand-off
     _lib.profile_reset(ctx)
     _lib.profile_enable(ctx, True)
+    K = args.steps
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    ev[0].record()
+    for i in range(K):
+        batch.step()
+        ev[i + 1].record()
     barrier()
     t1 = time.perf_counter()
     _lib.profile_enable(ctx, False)
     prof = _lib.profile_read(ctx)
+    _lib.synchronize(local)  # no map of the timed steps came from a given-up hand-off
     elapsed = t1 - t0
+    step_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(K)]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     if rank == 0:
-        K = args.steps
         ms_per_step = elapsed / K * 1e3
         mpix = world * F * W * H * K / elapsed / 1e6
         stages = {k: {"ms_per_step": v[0] / K, "launches_per_step": v[1] / K}
@@ -200,18 +322,26 @@ def main():
         kernels = [k for k in stages if not (k == "path_aggregation" and "path_strips" in stages)]
         dom = max(kernels, key=lambda k: stages[k]["ms_per_step"])
         launches = stages[dom]["launches_per_step"]
-        bytes_per_launch = int(stage_bytes(dom, F, W, H, W1, D, ndir, acc, strips) / launches)
         avg_launch_s = stages[dom]["ms_per_step"] / launches / 1e3
-        achieved = bytes_per_launch / avg_launch_s / 1e9
-        traffic = None
+        # SURVEY.md §8(d) compulsory bytes per frame (8 paths): u8 L+R in, int16
+        # map out, one int16 write + read of the cross-sweep aggregate per (px, d)
+        comp = 4 * W * H * (1 + D)
+        alg_bytes_per_launch = comp * F / launches
+        achieved = alg_bytes_per_launch / avg_launch_s / 1e9
+        impl_bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir, acc, strips) / launches
+        traffic, traffic_note = None, "no PMC summary for this workload"
         if os.path.exists(PMC_FILE):
             try:
                 pmc = json.load(open(PMC_FILE))
-                if pmc.get("workload") == f"sgbm_{W}x{H}_d{D}_{ndir}path_batch{F}":
+                if pmc.get("workload") != f"sgbm_{W}x{H}_d{D}_{ndir}path_batch{F}":
+                    traffic_note = "PMC summary is for another workload"
+                elif pmc.get("kernel_source_sha") != kernel_source_sha():
+                    traffic_note = "PMC summary is stale (kernel sources changed since)"
+                else:
                     traffic = pmc.get("stages", {}).get(dom, {}).get("hbm_bytes_per_launch")
+                    traffic_note = f"{os.path.relpath(PMC_FILE, ROOT)} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same kernel sources)"
             except (OSError, ValueError):
                 traffic = None
-        comp = 4 * W * H * (1 + D)  # SURVEY.md §8(d) compulsory bytes per frame, 8 paths
         res = {
             "metric": "Mpix disparities/sec (SGBM 128-disp, 8-path) at 1/2/4/8 GPUs; % HBM roofline",
             "value": round(mpix, 2),
@@ -220,6 +350,7 @@ def main():
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            "median_ms_per_step": round(statistics.median(step_ms), 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -231,32 +362,46 @@ def main():
                        "paths": ndir, "frames_per_gpu": F, "global_batch": F * world,
                        "params": "configs/sgbm.yml + mode", "gather": "rccl" if gather else "none",
                        "parallelism": f"frame-parallel x{world}"},
-            "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "roofline": {"kernel": dom, "bound": "hbm", "limiter": LIMITER.get(dom, ""),
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                         "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
+                         "traffic_source": traffic_note,
+                         "algorithmic_bytes_per_launch": int(alg_bytes_per_launch),
+                         "algorithmic_bytes": "SURVEY.md §8(d): 4*W*H*(1+D) per frame x frames per launch",
+                         "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                         "impl_bytes_per_launch": int(impl_bytes_per_launch),
+                         "impl_frac": round(impl_bytes_per_launch / avg_launch_s / 1e9 / HBM_PEAK_GBPS, 4)},
             "pipeline_compulsory": {"bytes_per_frame": comp,
                                     "achieved_GBps_per_gpu": round(comp * F * K / elapsed / 1e9, 1),
                                     "frac_of_peak": round(comp * F * K / elapsed / 1e9 / HBM_PEAK_GBPS, 5)},
             "stages_ms_per_step": {k: round(v["ms_per_step"], 4) for k, v in stages.items()},
         }
         if world == 1 and not args.no_cpu_baseline:
-            nf = min(args.cpu_frames, F)
-            thr = max(1, min(args.cpu_threads, nf))
-            wall, ref = cpu_baseline(host[:nf], params, thr)
-            gpu_out = out[:nf].cpu().numpy()
-            same = sum(int(np.array_equal(gpu_out[i], ref[i])) for i in range(nf))
-            res["cpu_baseline"] = {"value": round(nf * W * H / wall / 1e6, 3), "unit": "Mpix/s",
+            info = cpu_info()
+            thr = args.cpu_threads or max(1, min(CPU_SHARE, info["affinity"]))
+            # one frame per thread: the first F are the GPU's frames (parity sample)
+            seeds = [SEED0 + i for i in range(thr)]
+            frames = [host[i] if i < F else mvsv.synth_pair(seeds[i], W, H, minD, D)
+                      for i in range(thr)]
+            wall, ref = cpu_baseline(frames, params, thr)
+            lat, _ = cpu_baseline(frames[:1], params, 1)
+            nchk = min(F, thr)
+            gpu_out = out[:nchk].cpu().numpy()
+            same = sum(int(np.array_equal(gpu_out[i], ref[i])) for i in range(nchk))
+            res["cpu_baseline"] = {"value": round(thr * W * H / wall / 1e6, 3), "unit": "Mpix/s",
                                    "cores": thr, "kind": "port",
-                                   "sample": f"{nf} frames of the same workload, one frame per "
-                                             f"thread, scalar C oracle (OpenCV 3.4 restatement, "
-                                             f"no SIMD), {wall:.1f} s wall"}
-            res["parity_sample"] = f"{same}/{nf} frames bit-exact vs oracle"
+                                   "sample": f"{thr} frames of the same workload, one frame per "
+                                             f"thread on {thr} threads, scalar C oracle (OpenCV "
+                                             f"3.4 restatement, no SIMD -- slower than OpenCV's "
+                                             f"SSE2 path), {wall:.1f} s wall",
+                                   "latency_1core_s": round(lat, 3),
+                                   "host": info}
+            res["parity_sample"] = f"{same}/{nchk} frames bit-exact vs oracle"
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

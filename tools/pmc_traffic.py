@@ -11,8 +11,12 @@ raw and the corrected values are written; bench.py uses the corrected total.
 """
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_source_sha  # noqa: E402
 
 STAGES = [("sgbm_tri_kernel", "path_strips"), ("sgbm_path16_kernel", "path_lines"),
           ("sgbm_path_kernel", "path_aggregation"), ("sgbm_cost_fixup", "cost_fixup"),
@@ -69,6 +73,7 @@ def main(fetch_csv, write_csv, workload, out):
                       "hbm_bytes_per_launch": int(2 * fetch + write),
                       "hbm_bytes_per_launch_uncorrected": int(fetch + write)}
     json.dump({"workload": workload, "source": [fetch_csv, write_csv],
+               "kernel_source_sha": kernel_source_sha(),
                "correction": "fetch x2 (gfx950 FETCH_SIZE halving for wide streaming reads)",
                "stages": stages}, open(out, "w"), indent=1)
     print(json.dumps(stages, indent=1))
