@@ -273,6 +273,53 @@ MVSV_API int mvsv_init_undistort_rectify_map(const double* K, const double* dist
                                              int height, float* map_x, float* map_y,
                                              size_t map_stride);
 
+/* cv::stereoRectify(K1, D1, K2, D2, size, R, T, R1, R2, P1, P2, Q, flags, alpha,
+ * size, &roi1, &roi2) as Stereosystem::initRectification calls it
+ * (src/Stereosystem.cpp:209-212: flags = CALIB_ZERO_DISPARITY, alpha = 0).
+ * K 3x3, D (k1, k2, p1, p2[, k3[, k4, k5, k6]]), R 3x3, T 3; outputs R1/R2 3x3,
+ * P1/P2 3x4, Q 4x4 (may be NULL), valid-pixel ROIs (may be NULL); all row-major
+ * doubles.  Double-precision restatement of OpenCV 3.4's cvStereoRectify (host). */
+#define MVSV_CALIB_ZERO_DISPARITY 1024
+MVSV_API int mvsv_stereo_rectify(const double* K1, const double* D1, int ndist1, const double* K2,
+                                 const double* D2, int ndist2, int width, int height,
+                                 const double* R, const double* T, int flags, double alpha,
+                                 double* R1, double* R2, double* P1, double* P2, double* Q,
+                                 mvsv_rect* roi1, mvsv_rect* roi2);
+
+/* ---- calibration files -------------------------------------------
+ * cv::FileStorage YAML matrices ("key: !!opencv-matrix", rows / cols / dt / data) in
+ * the layout OpenCV 3.x writes (%YAML:1.0 header, data lists wrapped at column 71,
+ * doubles "%.16e", floats "%.8e", integral values "%d."): the files of
+ * parameters/<system>/{intrinsic,extrinsic}.yml and afterCalibrationParameters.yml.
+ * Empty matrices are rows = cols = 0, dt 'u'. */
+#define MVSV_MAT_MAX 16
+typedef struct {
+    int rows, cols;
+    char dt; /* 'u' 'c' 'w' 's' 'i' 'f' 'd' (CV_8U ... CV_64F) */
+    double data[MVSV_MAT_MAX];
+} mvsv_mat;
+/* Stereosystem's intrinsic state: the nodes saveIntrinsic writes, in order. */
+typedef struct {
+    mvsv_mat camera_matrix_left, camera_matrix_right, dist_coeffs_left, dist_coeffs_right,
+        camera_matrix_left_new, camera_matrix_right_new, q_matrix;
+} mvsv_intrinsics;
+typedef struct { mvsv_mat R, T, E, F; } mvsv_extrinsics;
+/* One matrix node: MVSV_E_IO (cannot open), MVSV_E_PARSE (absent / malformed / > 16). */
+MVSV_API int mvsv_read_matrix_yaml(const char* path, const char* key, mvsv_mat* out);
+/* n matrix nodes in order (a new file). */
+MVSV_API int mvsv_write_matrices_yaml(const char* path, const char* const* keys,
+                                      const mvsv_mat* mats, int n);
+/* Stereosystem::loadIntrinsic (src/Stereosystem.cpp:356-386): cameraMatrixLeft,
+ * cameraMatrixRight and distCoeffsRight must exist (the reference checks
+ * distCoeffsRight twice, never distCoeffsLeft); the *_new and Q fields come back
+ * empty (loadIntrinsic does not read them). */
+MVSV_API int mvsv_load_intrinsic(const char* path, mvsv_intrinsics* out);
+/* Stereosystem::loadExtrinisic (src/Stereosystem.cpp:326-354): R, T, E, F required. */
+MVSV_API int mvsv_load_extrinsic(const char* path, mvsv_extrinsics* out);
+/* Stereosystem::saveIntrinsic / saveExtrinsic (src/Stereosystem.cpp:388-446). */
+MVSV_API int mvsv_save_intrinsic(const char* path, const mvsv_intrinsics* in);
+MVSV_API int mvsv_save_extrinsic(const char* path, const mvsv_extrinsics* in);
+
 /* ---- after the path: reprojection and point-cloud output ----
  * Q is the 4x4 CV_32F reprojection matrix of stereoRectify, 16 floats row-major
  * (e.g. afterCalibrationParameters.yml "Q"). */

@@ -12,6 +12,7 @@ from ._lib import (MODE_HH, MODE_SGBM, MVSV_E_TIMEOUT, OPT_STRIP_SPIN_LIMIT,
 from .disparity import (Disparity, StereoBM, StereoSGBM, Stereopair, mean_disparity_grid,
                         sgbmParameters, synth_pair)
 from .detection import DisparityStream, MeanDisparityDetection, Subimage, create_dmap_rois
+from .calibration import Stereosystem, read_matrix, stereo_rectify, write_matrices
 from .rectify import init_undistort_rectify_map, rectify_pair, remap
 from .utility import Utility, dMapValues, ply, reproject
 
@@ -21,6 +22,7 @@ __all__ = [
     "PREFILTER_NORMALIZED_RESPONSE", "VARIANT_FIRSTCOL_FIX", "VARIANT_WTA_MIN_D",
     "DisparityStream", "MeanDisparityDetection", "Subimage", "create_dmap_rois", "Utility",
     "dMapValues", "ply", "reproject", "init_undistort_rectify_map", "rectify_pair", "remap",
-    "synchronize", "set_option", "MVSV_E_TIMEOUT", "OPT_STRIP_SPIN_LIMIT",
+    "synchronize", "set_option", "Stereosystem", "read_matrix", "write_matrices",
+    "stereo_rectify", "MVSV_E_TIMEOUT", "OPT_STRIP_SPIN_LIMIT",
 ]
 __version__ = "1.0.0"

@@ -555,162 +555,6 @@ int mvsv_bm(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* R, size_t
     return host_call(ctx, L, ls, R, rs, W, H, out, os, false, p);
 }
 
-// ---------------------------------------------------------------------------
-// Flat %YAML:1.0 "key: number" reader (the subset cv::FileStorage writes for
-// configs/sgbm.yml and configs/bm.yml). Numbers are rounded like cvRound.
-// ---------------------------------------------------------------------------
-static int read_flat_yaml(const char* path, std::map<std::string, double>* kv)
-{
-    if (!path) return MVSV_E_INVALID_ARG;
-    std::ifstream f(path);
-    if (!f.is_open()) return MVSV_E_IO;
-    std::string line;
-    bool first = true;
-    while (std::getline(f, line)) {
-        if (!line.empty() && line.back() == '\r') line.pop_back();
-        if (first) {
-            first = false;
-            if (line.rfind("%YAML", 0) == 0) continue;
-        }
-        size_t hash = line.find('#');
-        if (hash != std::string::npos) line = line.substr(0, hash);
-        if (line.find_first_not_of(" \t") == std::string::npos) continue;
-        if (line == "---" || line == "...") continue;
-        size_t colon = line.find(':');
-        if (colon == std::string::npos) continue;
-        std::string key = line.substr(0, colon);
-        std::string val = line.substr(colon + 1);
-        auto trim = [](std::string& s) {
-            size_t a = s.find_first_not_of(" \t\"'");
-            size_t b = s.find_last_not_of(" \t\"'");
-            s = a == std::string::npos ? std::string() : s.substr(a, b - a + 1);
-        };
-        trim(key);
-        trim(val);
-        if (key.empty() || val.empty()) continue;  // nested map / empty node
-        char* end = nullptr;
-        errno = 0;
-        double d = std::strtod(val.c_str(), &end);
-        if (end == val.c_str() || errno) continue;  // non-numeric: not an int node
-        (*kv)[key] = d;
-    }
-    return MVSV_OK;
-}
-
-static int kv_int(const std::map<std::string, double>& kv, const char* key, int dflt)
-{
-    auto it = kv.find(key);
-    return it == kv.end() ? dflt : (int)std::lrint(it->second);
-}
-
-int mvsv_load_sgbm_yaml(const char* path, mvsv_sgbm_params* p, mvsv_sgbm_yaml_values* v)
-{
-    std::map<std::string, double> kv;
-    int rc = read_flat_yaml(path, &kv);
-    if (rc) return rc;  // reference: LOG(ERROR) "Unable to open disparity parameters"
-    // src/disparity.cpp:67 — required nodes
-    for (const char* k : {"numDisp", "blockSize", "speckleWindowSize", "speckleWindowRange"})
-        if (!kv.count(k)) return MVSV_E_PARSE;
-    mvsv_sgbm_yaml_values tmp;
-    tmp.minDisp = kv_int(kv, "minDisp", 0);
-    tmp.numDisp = kv_int(kv, "numDisp", 0);
-    tmp.blockSize = kv_int(kv, "blockSize", 0);
-    tmp.disp12MaxDiff = kv_int(kv, "disp12MaxDiff", 0);
-    tmp.preFilterCap = kv_int(kv, "preFilterCap", 0);
-    tmp.uniquenessRatio = kv_int(kv, "uniquenessRatio", 0);
-    tmp.speckleWindowSize = kv_int(kv, "speckleWindowSize", 0);
-    tmp.speckleRange = kv_int(kv, "speckleWindowRange", 0);
-    tmp.disparityMode = kv_int(kv, "mode", 0);
-    if (v) *v = tmp;
-    if (p) {  // src/disparity.cpp:83-95 — eight setters + mode, P1/P2 untouched
-        p->min_disparity = tmp.minDisp;
-        p->num_disparities = tmp.numDisp;
-        p->block_size = tmp.blockSize;
-        p->pre_filter_cap = tmp.preFilterCap;
-        p->uniqueness_ratio = tmp.uniquenessRatio;
-        p->disp12_max_diff = tmp.disp12MaxDiff;
-        p->speckle_window_size = tmp.speckleWindowSize;
-        p->speckle_range = tmp.speckleRange;
-        p->mode = tmp.disparityMode == 1 ? MVSV_MODE_HH : MVSV_MODE_SGBM;
-    }
-    return MVSV_OK;
-}
-
-int mvsv_load_bm_yaml(const char* path, mvsv_bm_params* p)
-{
-    std::map<std::string, double> kv;
-    int rc = read_flat_yaml(path, &kv);
-    if (rc) return rc;
-    for (const char* k : {"numDisp", "blockSize"})
-        if (!kv.count(k)) return MVSV_E_PARSE;
-    if (p) {
-        p->num_disparities = kv_int(kv, "numDisp", p->num_disparities);
-        p->block_size = kv_int(kv, "blockSize", p->block_size);
-        p->pre_filter_cap = kv_int(kv, "preFilterCap", p->pre_filter_cap);
-        p->pre_filter_size = kv_int(kv, "preFilterSize", p->pre_filter_size);
-        p->uniqueness_ratio = kv_int(kv, "uniquenessRatio", p->uniqueness_ratio);
-        p->texture_threshold = kv_int(kv, "textureThreshold", p->texture_threshold);
-        p->min_disparity = kv_int(kv, "minDisp", p->min_disparity);
-        p->speckle_window_size = kv_int(kv, "speckleWindowSize", p->speckle_window_size);
-        p->speckle_range = kv_int(kv, "speckleWindowRange", p->speckle_range);
-        p->disp12_max_diff = kv_int(kv, "disp12MaxDiff", p->disp12_max_diff);
-        p->pre_filter_type = kv_int(kv, "preFilterType", p->pre_filter_type);
-    }
-    return MVSV_OK;
-}
-
-// ---------------------------------------------------------------------------
-// Synthetic rectified pair.
-// ---------------------------------------------------------------------------
-namespace {
-struct Pcg32 {
-    uint64_t state;
-    static constexpr uint64_t inc = 0xda3e39cb94b95bdbULL;
-    explicit Pcg32(uint32_t seed) : state((uint64_t)seed * 2u + 1u) {}
-    uint32_t next()
-    {
-        uint64_t old = state;
-        state = old * 6364136223846793005ULL + inc;
-        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
-        uint32_t rot = (uint32_t)(old >> 59u);
-        return (xs >> rot) | (xs << ((0u - rot) & 31u));
-    }
-};
-}  // namespace
-
-int mvsv_synth_pair(uint32_t seed, int W, int H, int minD, int D, uint8_t* Lout, uint8_t* Rout)
-{
-    if (W <= 0 || H <= 0 || D <= 0 || !Lout || !Rout) return MVSV_E_INVALID_ARG;
-    Pcg32 rng(seed);
-    size_t np = (size_t)W * H;
-    uint8_t* noise = (uint8_t*)std::malloc(np);
-    if (!noise) return MVSV_E_OOM;
-    for (size_t i = 0; i < np; i++) noise[i] = (uint8_t)(rng.next() >> 24);
-    for (int y = 0; y < H; y++)
-        for (int x = 0; x < W; x++) {
-            int s = 0;
-            for (int dy = -1; dy <= 1; dy++)
-                for (int dx = -1; dx <= 1; dx++) {
-                    int yy = std::min(std::max(y + dy, 0), H - 1);
-                    int xx = std::min(std::max(x + dx, 0), W - 1);
-                    s += noise[(size_t)yy * W + xx];
-                }
-            Lout[(size_t)y * W + x] = (uint8_t)((2 * s + 9) / 18);  // round half up of s/9
-        }
-    std::free(noise);
-    const int rect = (int)std::floor(0.6 * D + 0.5);
-    for (int y = 0; y < H; y++)
-        for (int x = 0; x < W; x++) {
-            bool in = x >= W / 3 && x < 2 * W / 3 && y >= H / 3 && y < 2 * H / 3;
-            int d = in ? rect : (int)std::floor(D / 8.0 + (D / 4.0) * y / H + 0.5);
-            d = std::min(std::max(d, minD), minD + D - 1);
-            int xs = std::min(std::max(x + d, 0), W - 1);
-            int v = Lout[(size_t)y * W + xs] + (int)(rng.next() % 3u) - 1;
-            Rout[(size_t)y * W + x] = (uint8_t)std::min(std::max(v, 0), 255);
-        }
-    return MVSV_OK;
-}
-
 }  // extern "C"
 
 // ---- reprojection and PLY output -------------------------
@@ -723,99 +567,6 @@ int mvsv_reproject_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, 
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad reprojection arguments");
     DeviceGuard dev_guard(ctx->device);
     return reproject_device(ctx, n, dmap, st, fs, W, H, Q, xyzw, xs, xfs);
-}
-
-// [Utility::calcCoordinate] src/utility.cpp:176-198 with OpenCV's float matrix
-// product (double accumulation, one rounding) and Mat /= w (float scale).
-void mvsv_calc_coordinate(float image_x, float image_y, float d_value, const float* Q, float* out)
-{
-    const float c[4] = {image_x, image_y, d_value / 16, 1.0f};
-    float r[4];
-    for (int i = 0; i < 4; i++) {
-        double acc = 0.0;
-        for (int k = 0; k < 4; k++) acc += (double)Q[4 * i + k] * (double)c[k];
-        r[i] = (float)acc;
-    }
-    const float alpha = (float)(1.0 / (double)r[3]);
-    for (int i = 0; i < 4; i++) out[i] = r[i] * alpha;
-    if (std::isinf(out[2] / 1000)) out[2] = 0.0f;
-}
-
-// [Utility::calcDistance] src/utility.cpp:200-222
-float mvsv_calc_distance(float image_x, float image_y, float d_value, const float* Q)
-{
-    const float c[4] = {image_x, image_y, d_value / 16, 1.0f};
-    float r[4];
-    for (int i = 0; i < 4; i++) {
-        double acc = 0.0;
-        for (int k = 0; k < 4; k++) acc += (double)Q[4 * i + k] * (double)c[k];
-        r[i] = (float)acc;
-    }
-    const float alpha = (float)(1.0 / (double)r[3]);
-    const float distance = (r[2] * alpha) / 1000;
-    return std::isinf(distance) ? 0.0f : distance;
-}
-
-// [Utility::calcDMapValues] src/utility.cpp:224-240
-void mvsv_calc_dmap_values(const float* c, const float* Q, float* image_x, float* image_y,
-                           float* d_value)
-{
-    const float numerator = Q[2 * 4 + 3] - c[2] * Q[3 * 4 + 3];
-    const float denominator = c[2] * Q[3 * 4 + 2];
-    const float disparity_value = numerator / denominator;
-    *image_x = c[0] * (disparity_value * Q[3 * 4 + 2] * Q[3 * 4 + 3]) + Q[0 * 4 + 3];
-    *image_y = c[1] * (disparity_value * Q[3 * 4 + 2] * Q[3 * 4 + 3]) + Q[1 * 4 + 3];
-    *d_value = disparity_value * 16;
-}
-
-// [Utility::calcMinMaxDisparity] src/utility.cpp:286-303 (positive values only)
-static bool min_max_positive(const int16_t* d, size_t st, int W, int H, short* mn, short* mx)
-{
-    bool any = false;
-    for (int r = 0; r < H; r++)
-        for (int c = 0; c < W; c++) {
-            const short v = d[(size_t)r * st + c];
-            if (v > 0) {
-                if (!any || v < *mn) *mn = v;
-                if (!any || v > *mx) *mx = v;
-                any = true;
-            }
-        }
-    return any;
-}
-
-// [ply::write] src/ply.cpp:37-133: std::ofstream with default float formatting
-int mvsv_write_ply(const char* path, const char* author, const char* object_name,
-                   const float* xyz, size_t count, size_t vstride, int mode, const int16_t* dmap,
-                   size_t dst, int W, int H)
-{
-    if (!path || (!xyz && count) || vstride < 3 || mode < MVSV_PLY_PLAIN ||
-        mode > MVSV_PLY_WITH_COLOR_SHADING)
-        return MVSV_E_INVALID_ARG;
-    short mn = 0, mx = 0;
-    if (mode != MVSV_PLY_PLAIN) {
-        if (!dmap || W <= 0 || H <= 0) return MVSV_E_INVALID_ARG;  // "mDMap.rows == 0" -> false
-        if (!min_max_positive(dmap, dst, W, H, &mn, &mx)) return MVSV_E_INVALID_ARG;
-    }
-    std::ofstream out(path);
-    if (!out) return MVSV_E_IO;
-    out << "ply\nformat ascii 1.0\ncomment author: " << (author ? author : "")
-        << "\ncomment object:" << (object_name ? object_name : "") << "\n";
-    out << "element vertex " << std::to_string(count) << "\n";
-    out << "property float x\nproperty float y\nproperty float z\n";
-    if (mode != MVSV_PLY_PLAIN) out << "property uchar red\nproperty uchar green\nproperty uchar blue\n";
-    out << "end_header\n";
-    for (size_t i = 0; i < count; i++) {
-        const float* t = xyz + i * vstride;
-        if (mode == MVSV_PLY_WITH_COLOR) {
-            out << t[0] << " " << t[1] << " " << t[2] << " ";
-            const int g = int((t[2] - mn) / (mx - mn) * 255.0);
-            out << g << " " << g << " " << g << "\n";
-        } else {
-            out << t[0] << " " << t[1] << " " << t[2] << "\n";
-        }
-    }
-    return out ? MVSV_OK : MVSV_E_IO;
 }
 
 // [Utility::dmap2pcl] src/utility.cpp:242-262
@@ -920,50 +671,3 @@ int mvsv_rectify_pair(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t*
     return check_hip(ctx, hipStreamSynchronize(s), "hipStreamSynchronize");
 }
 
-// [cv::initUndistortRectifyMap] (OpenCV 3.4 undistort.cpp), CV_32FC1 output
-int mvsv_init_undistort_rectify_map(const double* K, const double* dist, int ndist,
-                                    const double* Rm, const double* P, int W, int H, float* mx,
-                                    float* my, size_t ms)
-{
-    if (!K || !P || !mx || !my || W <= 0 || H <= 0 || ms < (size_t)W ||
-        !(ndist == 0 || ndist == 4 || ndist == 5 || ndist == 8) || (ndist && !dist))
-        return MVSV_E_INVALID_ARG;
-    const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    const double* R = Rm ? Rm : I3;
-    // A = P[:, :3] * R; iR = A^-1
-    double A[9];
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) {
-            double acc = 0;
-            for (int k = 0; k < 3; k++) acc += P[i * 3 + k] * R[k * 3 + j];
-            A[i * 3 + j] = acc;
-        }
-    const double det = A[0] * (A[4] * A[8] - A[5] * A[7]) - A[1] * (A[3] * A[8] - A[5] * A[6]) +
-                       A[2] * (A[3] * A[7] - A[4] * A[6]);
-    if (det == 0) return MVSV_E_INVALID_ARG;
-    double ir[9] = {(A[4] * A[8] - A[5] * A[7]) / det, (A[2] * A[7] - A[1] * A[8]) / det,
-                    (A[1] * A[5] - A[2] * A[4]) / det, (A[5] * A[6] - A[3] * A[8]) / det,
-                    (A[0] * A[8] - A[2] * A[6]) / det, (A[2] * A[3] - A[0] * A[5]) / det,
-                    (A[3] * A[7] - A[4] * A[6]) / det, (A[1] * A[6] - A[0] * A[7]) / det,
-                    (A[0] * A[4] - A[1] * A[3]) / det};
-    double k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = 0; i < ndist; i++) k[i] = dist[i];
-    const double k1 = k[0], k2 = k[1], p1 = k[2], p2 = k[3], k3 = k[4], k4 = k[5], k5 = k[6], k6 = k[7];
-    const double u0 = K[2], v0 = K[5], fx = K[0], fy = K[4];
-    for (int i = 0; i < H; i++) {
-        float* m1 = mx + (size_t)i * ms;
-        float* m2 = my + (size_t)i * ms;
-        double _x = i * ir[1] + ir[2], _y = i * ir[4] + ir[5], _w = i * ir[7] + ir[8];
-        for (int j = 0; j < W; j++, _x += ir[0], _y += ir[3], _w += ir[6]) {
-            const double w = 1. / _w, x = _x * w, y = _y * w;
-            const double x2 = x * x, y2 = y * y;
-            const double r2 = x2 + y2, _2xy = 2 * x * y;
-            const double kr = (1 + ((k3 * r2 + k2) * r2 + k1) * r2) / (1 + ((k6 * r2 + k5) * r2 + k4) * r2);
-            const double u = fx * (x * kr + p1 * _2xy + p2 * (r2 + 2 * x2)) + u0;
-            const double v = fy * (y * kr + p1 * (r2 + 2 * y2) + p2 * _2xy) + v0;
-            m1[j] = (float)u;
-            m2[j] = (float)v;
-        }
-    }
-    return MVSV_OK;
-}

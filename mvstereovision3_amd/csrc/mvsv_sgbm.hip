@@ -1217,14 +1217,22 @@ struct TriCfg {
     static constexpr int kSW = 4 * kWaves;  // U-columns per strip
     static constexpr int kThreads = 64 * (kWaves + 1);
 };
-constexpr int kTriPF = 2;               // steps of C prefetch (compute waves)
+#ifndef MVSV_TRI_PF
+#define MVSV_TRI_PF 4
+#endif
+constexpr int kTriPF = MVSV_TRI_PF;     // steps of C prefetch (compute waves)
 constexpr int kTriBF = 4;               // steps of boundary prefetch (comm wave)
 constexpr int kTriUnroll = 4;           // lcm(kTriPF, kTriBF, 2)
 
 template <int NP>
 struct TriLayout {
     static constexpr int kCols = TriCfg<NP>::kSW + 2;  // + two columns of the right strip
-    static constexpr int kColDw = 16 * NP;              // dwords per column
+    // dwords per column, odd: lane (column c, rl) reads / writes element p of
+    // its 2*NP disparities at c*kColDw + rl*NP + p, so for NP = 4 the 64 lanes
+    // of one b32 access hit 64 distinct banks (c + 4 rl + p mod 64); with the
+    // unpadded 16*NP stride the wave's 4 columns aliased onto the same 16
+    // banks (4-way conflicts on every neighbour read after the step barrier)
+    static constexpr int kColDw = 16 * NP + 1;
     static constexpr int kBufDw = 2 * kCols * kColDw;   // dirs b and c
     static constexpr int kLDw = 2 * kBufDw;             // double-buffered
     static constexpr int kMinInts = 2 * 2 * kCols;      // [buf][dir][col]
@@ -1293,7 +1301,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     constexpr int NG = TG::NG;
     constexpr int kTriWaves = TriCfg<NP>::kWaves;
     constexpr int kTriSW = TriCfg<NP>::kSW;
-    constexpr int PF = kTriPF;
+    constexpr int PF = NP >= 8 ? 2 : kTriPF;  // D = 256: 256 VGPRs already
     constexpr int BF = kTriBF;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* lds = (uint32_t*)smem;
@@ -1457,14 +1465,22 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     }
     __syncthreads();
 
+    // The exchange wave and the compute waves run separate loops with the same
+    // number of block barriers (one per step): the register allocator then
+    // gives each path its own registers (the exchange wave's granule prefetch
+    // no longer competes with the compute waves' C prefetch).
+    auto comm_step = [&](int i, int j) {
+        const int t = tb + i;
+        const int cur = i & 1, prv = cur ^ 1;
+        if (i > 0) publish(t - 1, prv);
+        bconsume(t, cur, bg[j % BF]);
+        bload(t + BF, bg[j % BF]);
+        __syncthreads();
+    };
     auto step = [&](int i, int j) {
         const int t = tb + i;
         const int cur = i & 1, prv = cur ^ 1;
-        if (comm) {
-            if (i > 0) publish(t - 1, prv);
-            bconsume(t, cur, bg[j % BF]);
-            bload(t + BF, bg[j % BF]);
-        } else {
+        {
             const int x = cell_x(t);
             const bool valid = x >= 0 && x < W1;
             uint32_t c[NP];
@@ -1524,13 +1540,23 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     };
     const int len = te - tb;
     int i = 0;
-    for (; i + kTriUnroll <= len; i += kTriUnroll) {
+    if (comm) {
+        for (; i + kTriUnroll <= len; i += kTriUnroll) {
 #pragma unroll
-        for (int j = 0; j < kTriUnroll; j++) step(i + j, j);
+            for (int j = 0; j < kTriUnroll; j++) comm_step(i + j, j);
+        }
+#pragma unroll
+        for (int j = 0; j < kTriUnroll; j++)
+            if (i + j < len) comm_step(i + j, j);
+    } else {
+        for (; i + kTriUnroll <= len; i += kTriUnroll) {
+#pragma unroll
+            for (int j = 0; j < kTriUnroll; j++) step(i + j, j);
+        }
+#pragma unroll
+        for (int j = 0; j < kTriUnroll; j++)
+            if (i + j < len) step(i + j, j);
     }
-#pragma unroll
-    for (int j = 0; j < kTriUnroll; j++)
-        if (i + j < len) step(i + j, j);
     if (comm) {
         publish(te - 1, (len - 1) & 1);
         if (stats && lane == 0) {

@@ -510,3 +510,26 @@ def test_rectify_pair_then_sgbm(gpu, mvsv, oracle):
     p = dict(mvsv.StereoSGBM.create(0, 32, 5).params())
     p.pop("variant")
     assert np.array_equal(d, oracle.sgbm(rl, rr, p))
+
+
+def test_stereosystem_rectified_pair_then_sgbm(gpu, mvsv, oracle):
+    """Stereosystem::initRectification (stereoRectify + initUndistortRectifyMap from the
+    reference's baseline_small calibration files, binning) + getRectifiedImagepair on
+    the GPU + Disparity::sgbm of the cropped pair, each step against the oracle."""
+    import os
+    cal = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "calib", "baseline_small")
+    s = mvsv.Stereosystem(376, 240, binning=True)
+    assert s.loadIntrinsic(os.path.join(cal, "intrinsic.yml"))
+    assert s.loadExtrinisic(os.path.join(cal, "extrinsic.yml"))
+    assert s.initRectification()
+    L, R = mvsv.synth_pair(SEED0 + 70, 376, 240, 0, 64)
+    sip = mvsv.Stereopair(L, R)
+    assert s.getRectifiedImagepair(sip)
+    x0, y0, x1, y1 = s.mDisplayROI
+    assert np.array_equal(sip.mLeft, oracle.remap_linear(L, s.mMap1[0], s.mMap2[0])[y0:y1, x0:x1])
+    assert np.array_equal(sip.mRight, oracle.remap_linear(R, s.mMap1[1], s.mMap2[1])[y0:y1, x0:x1])
+    m = mvsv.StereoSGBM.create(0, 64, 9, 8 * 81, 32 * 81)
+    d = m.compute(sip.mLeft, sip.mRight)
+    p = dict(m.params())
+    p.pop("variant")
+    assert np.array_equal(d, oracle.sgbm(np.ascontiguousarray(sip.mLeft), np.ascontiguousarray(sip.mRight), p))
