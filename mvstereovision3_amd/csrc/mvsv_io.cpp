@@ -21,6 +21,49 @@
 
 extern "C" {
 
+int mvsv_version(void) { return MVSV_VERSION; }
+
+void mvsv_sgbm_params_create(mvsv_sgbm_params* p, int min_disparity, int num_disparities,
+                             int block_size, int p1, int p2, int disp12_max_diff,
+                             int pre_filter_cap, int uniqueness_ratio, int speckle_window_size,
+                             int speckle_range, int mode)
+{
+    if (!p) return;
+    p->min_disparity = min_disparity;
+    p->num_disparities = num_disparities;
+    p->block_size = block_size;
+    p->p1 = p1;
+    p->p2 = p2;
+    p->disp12_max_diff = disp12_max_diff;
+    p->pre_filter_cap = pre_filter_cap;
+    p->uniqueness_ratio = uniqueness_ratio;
+    p->speckle_window_size = speckle_window_size;
+    p->speckle_range = speckle_range;
+    p->mode = mode;
+    p->variant = 0;
+}
+
+void mvsv_sgbm_params_default(mvsv_sgbm_params* p)
+{
+    mvsv_sgbm_params_create(p, 0, 16, 3, 0, 0, 0, 0, 0, 0, 0, MVSV_MODE_SGBM);
+}
+
+void mvsv_bm_params_default(mvsv_bm_params* p, int num_disparities, int block_size)
+{
+    if (!p) return;
+    p->pre_filter_type = MVSV_PREFILTER_XSOBEL;
+    p->pre_filter_size = 9;
+    p->pre_filter_cap = 31;
+    p->block_size = block_size;
+    p->min_disparity = 0;
+    p->num_disparities = num_disparities > 0 ? num_disparities : 64;
+    p->texture_threshold = 10;
+    p->uniqueness_ratio = 15;
+    p->speckle_window_size = 0;
+    p->speckle_range = 0;
+    p->disp12_max_diff = -1;
+}
+
 // ---------------------------------------------------------------------------
 // Flat %YAML:1.0 "key: number" reader (the subset cv::FileStorage writes for
 // configs/sgbm.yml and configs/bm.yml). Numbers are rounded like cvRound.

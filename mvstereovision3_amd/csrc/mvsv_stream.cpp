@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "mvsv_internal.hpp"
+#include "mvsv_ring.hpp"
 
 using namespace mvsv;
 
@@ -139,9 +140,10 @@ static int stream_launch(mvsv_stream* st)
     const size_t px = (size_t)W * H;
     const long depth = (long)st->slots.size();
     int rc;
-    while (st->launched < st->head) {
-        const long i0 = st->launched % depth;
-        const int n = (int)std::min(st->head - st->launched, depth - i0);
+    RingRun run;
+    while (ring_next_run(st->launched, st->head, depth, &run)) {
+        const long i0 = run.i0;
+        const int n = run.n;
         auto& first = st->slots[i0];
         auto& last = st->slots[i0 + n - 1];
         // the upload stream is in order: the last slot's upload covers the run
@@ -213,7 +215,7 @@ int mvsv_stream_push(mvsv_stream* st, const uint8_t* L, size_t ls, const uint8_t
     mvsv_ctx* ctx = st->ctx;
     if (!L || !R || ls < (size_t)st->W || rs < (size_t)st->W)
         return set_error(ctx, MVSV_E_INVALID_ARG, "null frame or stride smaller than width");
-    if (st->head - st->tail >= (long)st->slots.size())
+    if (ring_full(st->head, st->tail, (long)st->slots.size()))
         return set_error(ctx, MVSV_E_INVALID_ARG, "stream full: pop a frame first");
     DeviceGuard dev_guard(ctx->device);
     auto& s = st->slots[st->head % st->slots.size()];
@@ -231,7 +233,7 @@ int mvsv_stream_push(mvsv_stream* st, const uint8_t* L, size_t ls, const uint8_t
         return rc;
     st->head++;
     // a full group, or a group that would otherwise wrap past the ring's end
-    if (st->head - st->launched >= st->batch || st->head % (long)st->slots.size() == 0)
+    if (ring_launch_after_push(st->head, st->launched, st->batch, (long)st->slots.size()))
         return stream_launch(st);
     return MVSV_OK;
 }

@@ -618,7 +618,7 @@ static void bm_stripe(const uint8_t* Lf, const uint8_t* Rf, int W, int H, int ro
     const int width = W, height = row1 - row0;
     const int width1 = width - rofs - ndisp + 1;
     const int ftzero = p->pre_filter_cap;
-    const int16_t FILTERED = (int16_t)((mindisp - 1) << DISP_SHIFT);
+    const int16_t FILTERED = (int16_t)((mindisp - 1) * (1 << DISP_SHIFT));  /* no UB shift of a negative value */
     const int nrow = height + dy0 + dy1;
     /* hsad[y + dy0][d], cbuf[ring][y + dy0][d], htext[y + wsz2 + 1] */
     int* hsad0 = (int*)calloc((size_t)nrow * ndisp, sizeof(int));
@@ -771,7 +771,7 @@ int orc_bm_compute(const uint8_t* L, ptrdiff_t ls, const uint8_t* R, ptrdiff_t r
     if (p->texture_threshold < 0 || p->uniqueness_ratio < 0) return -2;
 
     const int ndisp = p->num_disparities, mindisp = p->min_disparity;
-    const int16_t FILTERED = (int16_t)((mindisp - 1) << DISP_SHIFT);
+    const int16_t FILTERED = (int16_t)((mindisp - 1) * (1 << DISP_SHIFT));  /* no UB shift of a negative value */
     int lofs = imax(ndisp - 1 + mindisp, 0), rofs = -imin(ndisp - 1 + mindisp, 0);
     int width1 = W - rofs - ndisp + 1;
     if (lofs >= W || rofs >= W || width1 < 1) {
