@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include "mvsv_cost_layout.hpp"
 #include "mvsv_device.hpp"
 #include "mvsv_internal.hpp"
 
@@ -317,48 +318,6 @@ __global__ __launch_bounds__(256) void sgbm_cost_kernel(const uint64_t* __restri
 //          NR, resolved at compile time by unrolling the row loop by NR).
 // One workgroup barrier per row.
 // ---------------------------------------------------------------------------
-constexpr int kCost2Threads = 512;
-constexpr int kCost2Run = 4;
-
-struct Cost2Layout {
-    int PP, CL, TX, TY, NX, PS, nQmax, qhalf;
-    size_t off_l4, off_l2, off_q4, off_q2, off_pix, bytes;
-    size_t lstride4, lstride2, qstride4, qstride2, pstride;  // bytes per buffer (x2 each)
-};
-
-// A column's BT operands for both channels are six u16-pair dwords
-// {a.v, a.lo, a.hi, b.v, b.lo, b.hi}: dwords 0-3 in a 16-byte slot (ds_read_b128,
-// 4 LDS cycles), dwords 4-5 in an 8-byte slot (ds_read_b64, 2 cycles).  Right
-// pairs j are stored by parity so the lanes of a wave (j = t + 2p) read
-// consecutive, conflict-free slots.
-__host__ __device__ inline Cost2Layout cost2_layout(int D, int SW2, int TY)
-{
-    Cost2Layout c;
-    c.PP = D / 2;
-    c.CL = kCost2Threads / c.PP;
-    c.TX = c.CL * kCost2Run;
-    c.TY = TY;
-    c.NX = c.TX + 2 * SW2;  // even
-    // pix row: [pair p][column], PS dwords per pair with PS/2 odd: the b64
-    // column-pair stores (16-lane groups, 32 banks) and the b64 window loads
-    // (32-lane groups, 64 banks) of a wave are conflict-free
-    c.PS = c.NX + ((2 - c.NX) % 4 + 4) % 4;
-    c.nQmax = c.NX + D - 1;
-    c.qhalf = (c.nQmax + 1) / 2;  // slots per parity half
-    c.lstride4 = (size_t)c.NX * 16;
-    c.lstride2 = (size_t)c.NX * 8;
-    c.qstride4 = (size_t)2 * c.qhalf * 16;
-    c.qstride2 = (size_t)2 * c.qhalf * 8;
-    c.pstride = (size_t)c.PS * c.PP * 4;
-    c.off_l4 = 0;
-    c.off_q4 = c.off_l4 + 2 * c.lstride4;
-    c.off_l2 = c.off_q4 + 2 * c.qstride4;
-    c.off_q2 = c.off_l2 + 2 * c.lstride2;
-    c.off_pix = ((c.off_q2 + 2 * c.qstride2) + 15) & ~(size_t)15;
-    c.bytes = c.off_pix + 2 * c.pstride;
-    return c;
-}
-
 // broadcast form of one channel dword (bytes v, lo, hi): {v|v<<16, lo|lo<<16, hi|hi<<16}
 __device__ __forceinline__ uint3 bt_bcast(uint32_t w)
 {
@@ -396,13 +355,9 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
     const int PP = PPC > 0 ? PPC : lay.PP, CL = PPC > 0 ? kCost2Threads / PPC : lay.CL;
     const int TX = CL * kCost2Run, NX = lay.NX;
     const int f = blockIdx.z;
-    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
-    const int y1 = min(y0 + TY, H);
-    const int xclo = max(x0 - SW2, 0), xchi = min(x0 + TX + SW2 - 1, W1 - 1);
-    const int nL = xchi - xclo + 1;
-    const int nQ = nL + D - 1;
-    const int ilo = e.minX1 + xclo;
-    const int rtop = e.minX1 + xchi - e.minD;  // right column of reversed item j = 0
+    const Cost2Tile tile = cost2_tile(TX, TY, SW2, blockIdx.x, blockIdx.y, W1, H, e.minX1, e.minD, D);
+    const int x0 = tile.x0, y0 = tile.y0, y1 = tile.y1, xclo = tile.xclo;
+    const int nL = tile.nL;
     const size_t plane = (size_t)W * H;
     const uint64_t* PL = pre + (size_t)f * 2 * plane;
     const int tid = threadIdx.x;
@@ -410,9 +365,8 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
     const bool worker = cl < CL;
     const int tx0 = cl * kCost2Run;
     const uint32_t p2x2 = (uint32_t)(e.P2 & 0xffff) * 0x10001u;
-    const int nItems = nL + nQ;
-    // no clamped columns in this tile
-    const bool linear = x0 - SW2 >= 0 && x0 + TX + SW2 <= W1;
+    const int nItems = tile.nItems;
+    const bool linear = tile.linear;  // no clamped columns in this tile
 
     // staging: item i < nL -> left column ilo + i; else right pair j = i - nL
     // (reversed columns rtop - j and rtop - j - 1, zero outside the image).
@@ -427,14 +381,11 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
     for (int k = 0; k < STG; k++) {
         const int i = kCost2Threads - 1 - tid + kCost2Threads * k;  // high waves: fewer pix columns
-        const bool left = i < nL;
-        const int xa = left ? ilo + i : rtop - (i - nL);
-        const int xb = xa - 1;
-        ma[k] = i < nItems && xa >= 0 && xa < W;
-        mb[k] = !left && i < nItems && xb >= 0 && xb < W;
-        const int pofs = left ? 0 : (int)plane;  // right plane follows the left one
-        oa[k] = pofs + clampi(xa, 0, W - 1);
-        ob[k] = pofs + clampi(xb, 0, W - 1);
+        const Cost2Item it = cost2_item(tile, i, W, (int)plane);
+        ma[k] = it.ma;
+        mb[k] = it.mb;
+        oa[k] = it.oa;
+        ob[k] = it.ob;
     }
     auto fetch_row = [&](int v) {
         const uint64_t* row = PL + (size_t)clampi(v, 0, H - 1) * W;
@@ -458,8 +409,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                 l4[i] = make_uint4(fa.x, fa.y, fa.z, fb.x);
                 l2[i] = make_uint2(fb.y, fb.z);
             } else if (i < nItems) {
-                const int j = i - nL;
-                const int q = (j & 1) * lay.qhalf + lay.qhalf - 1 - (j >> 1);  // descending
+                const int q = cost2_qslot(lay, i - nL);  // descending
                 const uint3 fa = bt_pairform((uint32_t)va, (uint32_t)vb);
                 const uint3 fb = bt_pairform((uint32_t)(va >> 32), (uint32_t)(vb >> 32));
                 q4[q] = make_uint4(fa.x, fa.y, fa.z, fb.x);
@@ -476,7 +426,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
         if (!worker) return;
         // slot of right pair j = t + 2p (t = xchi - xc); slots descend with j, so
         // a column lane's slot ascends as its column xv does
-        auto qslot = [&](int t) { return (t & 1) * lay.qhalf + lay.qhalf - 1 - (t >> 1) - p; };
+        auto qslot = [&](int t) { return cost2_qslot(lay, t + 2 * p); };
         // column lane cl computes column pairs (xv, xv + 1), xv = 2 cl + 2 CL k,
         // and stores each pair with one b64 write
         if (linear) {
