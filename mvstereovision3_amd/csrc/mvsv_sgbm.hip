@@ -28,6 +28,10 @@
 #include "mvsv_device.hpp"
 #include "mvsv_internal.hpp"
 
+#ifndef MVSV_COST2_FETCH_DEPTH
+#define MVSV_COST2_FETCH_DEPTH 1  // staged rows in flight in the cost kernel (A/B knob)
+#endif
+
 namespace mvsv {
 namespace {
 
@@ -375,7 +379,10 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
     // only issues loads, and the loaded words are first touched by the next
     // row's stage_row -- so each row's loads stay in flight for a whole row
     // interval instead of being waited for where they are issued.
-    uint64_t pa[STG], pb[STG];
+    // staged rows in flight: row r's loads sit in register set r % FD and are
+    // first used FD - 1 rows after the row that issued them
+    constexpr int FD = MVSV_COST2_FETCH_DEPTH;
+    uint64_t pa[FD][STG], pb[FD][STG];
     int oa[STG], ob[STG];
     bool ma[STG], mb[STG];
 #pragma unroll
@@ -387,15 +394,15 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
         oa[k] = it.oa;
         ob[k] = it.ob;
     }
-    auto fetch_row = [&](int v) {
+    auto fetch_row = [&](int v, int set) {
         const uint64_t* row = PL + (size_t)clampi(v, 0, H - 1) * W;
 #pragma unroll
         for (int k = 0; k < STG; k++) {
-            pa[k] = row[oa[k]];
-            pb[k] = row[ob[k]];
+            pa[set][k] = row[oa[k]];
+            pb[set][k] = row[ob[k]];
         }
     };
-    auto stage_row = [&](int buf) {
+    auto stage_row = [&](int buf, int set) {
         uint4* l4 = (uint4*)(smem + lay.off_l4 + (buf ? lay.lstride4 : 0));
         uint2* l2 = (uint2*)(smem + lay.off_l2 + (buf ? lay.lstride2 : 0));
         uint4* q4 = (uint4*)(smem + lay.off_q4 + (buf ? lay.qstride4 : 0));
@@ -403,7 +410,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
         for (int k = 0; k < STG; k++) {
             const int i = kCost2Threads - 1 - tid + kCost2Threads * k;  // high waves: fewer pix columns
-            const uint64_t va = ma[k] ? pa[k] : 0ull, vb = mb[k] ? pb[k] : 0ull;
+            const uint64_t va = ma[k] ? pa[set][k] : 0ull, vb = mb[k] ? pb[set][k] : 0ull;
             if (i < nL) {
                 const uint3 fa = bt_bcast((uint32_t)va), fb = bt_bcast((uint32_t)(va >> 32));
                 l4[i] = make_uint4(fa.x, fa.y, fa.z, fb.x);
@@ -504,19 +511,24 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
     const bool hh_pin = e.fullDP != 0;  // the fix-up kernel's MODE_HH cases, done here
     const bool fix_x0 = (e.variant & MVSV_VARIANT_FIRSTCOL_FIX) != 0;
     const int ybot = max(H - SH2, 1);
-    fetch_row(vstart);
-    stage_row(0);
-    if (nrows > 1) fetch_row(vstart + 1);
-    __syncthreads();
-    for (int base = 0; base < nrows; base += NR) {
+    fetch_row(vstart, 0);
+    stage_row(0, 0);
 #pragma unroll
-        for (int s = 0; s < NR; s++) {
-            const int k = base + s;
+    for (int r = 1; r <= FD; r++)
+        if (r < nrows) fetch_row(vstart + r, r % FD);
+    __syncthreads();
+    // unrolled by NR * FD: the ring slot (k mod NR) and the register set of
+    // every staged row are compile-time constants
+    for (int base = 0; base < nrows; base += NR * FD) {
+#pragma unroll
+        for (int su = 0; su < NR * FD; su++) {
+            const int k = base + su;
+            const int s = su % NR;
             if (k >= nrows) break;
             const int buf = k & 1;
             if (k + 1 < nrows) {
-                stage_row(buf ^ 1);
-                if (k + 2 < nrows) fetch_row(vstart + k + 2);
+                stage_row(buf ^ 1, (su + 1) % FD);
+                if (k + 1 + FD < nrows) fetch_row(vstart + k + 1 + FD, (su + 1) % FD);
             }
             pix_row(buf);
             __syncthreads();  // pix[buf] complete; staging of row k+1 visible
@@ -1008,7 +1020,39 @@ __device__ __forceinline__ void sgm_step_row(const uint32_t (&lp)[NP], uint32_t 
 // in [minLp, minLp + P2]).  The neighbour minima min(L[d-1], L[d+1]) of the
 // NP pairs come from NP + 1 pairwise minima X_q = min(pair q, pair q + 1):
 // pair p's is (X_{p-1}.hi, X_p.lo) -- one v_pk_min + one v_alignbit per pair.
-template <int NP>
+//
+// NW ("no wrap", chosen by the host when P2 + blockSize^2 * (2*ftzero + 63) +
+// P2 <= 32767, sgbm_no_wrap): every C, L and delta = minLp + P2 is then a
+// non-negative int16, so with u = delta - min(m, delta) = max(delta - m, 0)
+// (one unsigned saturating subtract) L = C - u, and the path's increment over
+// cb is P2 - u: five VALU per pair instead of six.  tu[] returns u (NW) or the
+// signed t = -u (the general form, exact for wrapped costs too).
+template <bool NW>
+__device__ __forceinline__ void sgm_pair(uint32_t lp, uint32_t nb, uint32_t delta2, uint32_t p1x2,
+                                         uint32_t c, uint32_t& ln, uint32_t& tu)
+{
+    const uint32_t m = pk_min(lp, pk_add_sat(nb, p1x2));
+    if constexpr (NW) {
+        tu = pk_subsat_u16(delta2, m);
+        ln = pk_sub_sat(c, tu);
+    } else {
+        tu = pk_sub_sat(pk_min(m, delta2), delta2);
+        ln = pk_add_sat(tu, c);
+    }
+}
+// delta = t + P2 (general) = P2 - u (NW), in [0, P2]
+template <bool NW>
+__device__ __forceinline__ uint32_t sgm_delta(uint32_t tu, uint32_t p2x2)
+{
+    return NW ? pk_sub_u16(p2x2, tu) : pk_add_u16(tu, p2x2);
+}
+// the packed delta = (short)(minLp + P2) of the next step
+template <bool NW>
+__device__ __forceinline__ uint32_t sgm_delta2(int minp, int P2)
+{
+    return NW ? (uint32_t)(minp + P2) * 0x10001u : (uint32_t)((minp + P2) & 0xffff) * 0x10001u;
+}
+template <int NP, bool NW = false>
 __device__ __forceinline__ void sgm_step_row_t(const uint32_t (&lp)[NP], uint32_t delta2,
                                                uint32_t p1x2, const uint32_t (&c)[NP],
                                                uint32_t (&ln)[NP], uint32_t (&t)[NP])
@@ -1027,13 +1071,8 @@ __device__ __forceinline__ void sgm_step_row_t(const uint32_t (&lp)[NP], uint32_
     for (int q = 0; q + 1 < NP; q++) X[q + 1] = pk_min(lp[q], lp[q + 1]);
     X[NP] = pk_min(lp[NP - 1], next_lo);
 #pragma unroll
-    for (int p = 0; p < NP; p++) {
-        const uint32_t nb = __builtin_amdgcn_alignbit(X[p + 1], X[p], 16);
-        uint32_t m = pk_min(lp[p], pk_add_sat(nb, p1x2));
-        m = pk_min(m, delta2);
-        t[p] = pk_sub_sat(m, delta2);
-        ln[p] = pk_add_sat(t[p], c[p]);
-    }
+    for (int p = 0; p < NP; p++)
+        sgm_pair<NW>(lp[p], __builtin_amdgcn_alignbit(X[p + 1], X[p], 16), delta2, p1x2, c[p], ln[p], t[p]);
 }
 
 template <int NP>
@@ -1064,7 +1103,7 @@ __device__ __forceinline__ uint32_t row_min_u16x2(uint32_t v)
 
 constexpr int kPath16PF = 12;
 
-template <int NP, bool FIRST, typename AccT>
+template <int NP, bool FIRST, typename AccT, bool NW = false>
 __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restrict__ C,
                                                           AccT* __restrict__ A,
                                                           AccT* __restrict__ dummy, int H, int W1,
@@ -1107,16 +1146,15 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
         if constexpr (!FIRST) AV::load(acc_add(ap, t * step), ab[j]);
     }
     auto body = [&](int s, int j) {
-        const int dl = (int16_t)(minp + P2);
-        const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
+        const uint32_t delta2 = sgm_delta2<NW>(minp, P2);
         uint32_t c[NP], ln[NP], o[NP], tt[NP];
 #pragma unroll
         for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
-        sgm_step_row_t<NP>(lp, delta2, p1x2, c, ln, tt);
+        sgm_step_row_t<NP, NW>(lp, delta2, p1x2, c, ln, tt);
         minp = row_min_i32(lane_min_row<NP>(ln));
 #pragma unroll
         for (int p = 0; p < NP; p++) {
-            const uint32_t dv = pk_add_u16(tt[p], p2x2);  // delta = t + P2
+            const uint32_t dv = sgm_delta<NW>(tt[p], p2x2);  // delta = t + P2 = P2 - u
             if constexpr (FIRST)
                 o[p] = dv;
             else
@@ -1237,7 +1275,7 @@ __device__ __forceinline__ size_t tri_slot(int chain, int k, int t, int nchains,
     return ((((size_t)k * nchains + chain) * H + t) * 4) * 16 * TriGran<NP>::NG;
 }
 
-template <int NP, typename AccT>
+template <int NP, typename AccT, bool NW = false>
 __global__ __launch_bounds__(TriCfg<NP>::kThreads)
 __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     const int16_t* __restrict__ C, AccT* __restrict__ A, size_t plane, AccT* __restrict__ dummy,
@@ -1449,9 +1487,9 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
             }
             const int mb = *mcol(prv, 0, col + 1), mc = *mcol(prv, 1, col + 2);
             uint32_t na[NP], nb[NP], nc[NP], ta[NP], tb_[NP], tc[NP];
-            sgm_step_row_t<NP>(la, (uint32_t)((ma + P2) & 0xffff) * 0x10001u, p1x2, c, na, ta);
-            sgm_step_row_t<NP>(pb, (uint32_t)((mb + P2) & 0xffff) * 0x10001u, p1x2, c, nb, tb_);
-            sgm_step_row_t<NP>(pc, (uint32_t)((mc + P2) & 0xffff) * 0x10001u, p1x2, c, nc, tc);
+            sgm_step_row_t<NP, NW>(la, sgm_delta2<NW>(ma, P2), p1x2, c, na, ta);
+            sgm_step_row_t<NP, NW>(pb, sgm_delta2<NW>(mb, P2), p1x2, c, nb, tb_);
+            sgm_step_row_t<NP, NW>(pc, sgm_delta2<NW>(mc, P2), p1x2, c, nc, tc);
             const int mna = row_min_i32(lane_min_row<NP>(na));
             // DPP-folded i32 row minima (v_min_i32_dpp): one op per butterfly step
             const int mnb = row_min_i32(lane_min_row<NP>(nb));
@@ -1459,8 +1497,12 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
             uint32_t o[NP];
 #pragma unroll
             for (int p = 0; p < NP; p++) {
-                // sum of the three deltas t_r + P2, exact in u16 wrap arithmetic
-                o[p] = pk_add_u16(pk_add_u16(ta[p], tb_[p]), pk_add_u16(tc[p], p2x3));
+                // sum of the three deltas t_r + P2 = 3 P2 - (u_a + u_b + u_c),
+                // exact in u16 wrap arithmetic
+                if constexpr (NW)
+                    o[p] = pk_sub_u16(p2x3, pk_add_u16(pk_add_u16(ta[p], tb_[p]), tc[p]));
+                else
+                    o[p] = pk_add_u16(pk_add_u16(ta[p], tb_[p]), pk_add_u16(tc[p], p2x3));
             }
             AV::store(valid ? acc_addu(Af, cell_off(t)) : dp, o);
             if (__builtin_expect(!__all(valid), 0)) {
@@ -1668,14 +1710,14 @@ __device__ __forceinline__ int seg_min_i32(int v)
 // sgm_step_row_t over an LPR-lane segment: the d-1 / d+1 neighbours of a lane's
 // first / last pair come from the adjacent lane of the segment (MAX at the
 // segment ends).
-template <int NP, int LPR>
+template <int NP, int LPR, bool NW>
 __device__ __forceinline__ void sgm_step_seg_t(const uint32_t (&lp)[NP], uint32_t delta2,
                                                uint32_t p1x2, const uint32_t (&c)[NP],
                                                uint32_t (&ln)[NP], uint32_t (&t)[NP], bool seg_first,
                                                bool seg_last)
 {
     if constexpr (LPR == 16) {
-        sgm_step_row_t<NP>(lp, delta2, p1x2, c, ln, t);
+        sgm_step_row_t<NP, NW>(lp, delta2, p1x2, c, ln, t);
     } else {
         const uint32_t MAXP = 0x7fff7fffu;
         // zero-filled wave shifts (bound_ctrl) OR'ed with MAX at the segment
@@ -1691,13 +1733,9 @@ __device__ __forceinline__ void sgm_step_seg_t(const uint32_t (&lp)[NP], uint32_
         for (int q = 0; q + 1 < NP; q++) X[q + 1] = pk_min(lp[q], lp[q + 1]);
         X[NP] = pk_min(lp[NP - 1], next_lo);
 #pragma unroll
-        for (int p = 0; p < NP; p++) {
-            const uint32_t nb = __builtin_amdgcn_alignbit(X[p + 1], X[p], 16);
-            uint32_t m = pk_min(lp[p], pk_add_sat(nb, p1x2));
-            m = pk_min(m, delta2);
-            t[p] = pk_sub_sat(m, delta2);
-            ln[p] = pk_add_sat(t[p], c[p]);
-        }
+        for (int p = 0; p < NP; p++)
+            sgm_pair<NW>(lp[p], __builtin_amdgcn_alignbit(X[p + 1], X[p], 16), delta2, p1x2, c[p], ln[p],
+                         t[p]);
     }
 }
 
@@ -1750,7 +1788,7 @@ __device__ __forceinline__ uint32_t pk_mad_u16_clamp(uint32_t a, uint32_t b, uin
 // NACC accumulator planes (A + i * plane) hold the summed deltas of disjoint
 // direction groups written by concurrent passes; their sum is the S input.
 // UQ: uniquenessRatio > 0.
-template <int NP, int NACC, typename AccT, bool UQ, int LPR>
+template <int NP, int NACC, typename AccT, bool UQ, int LPR, bool NOWRAP = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 : 2))) void sgbm_final16_kernel(const int16_t* __restrict__ C,
                                                          const AccT* __restrict__ A, size_t plane,
                                                          int H, int W, SgbmEff e,
@@ -1852,12 +1890,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     __shared__ uint2 srec[RPW * LPR];
     uint2* recs = srec + row * LPR;
     auto body = [&](int s, int j) {
-        const int dl = (int16_t)(minp + e.P2);
-        const uint32_t delta2 = (uint32_t)(dl & 0xffff) * 0x10001u;
+        const uint32_t delta2 = sgm_delta2<NOWRAP>(minp, e.P2);
         uint32_t c[NP], ln[NP], st[NP], acc[NP], tt[NP];
 #pragma unroll
         for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
-        sgm_step_seg_t<NP, LPR>(lp, delta2, p1x2, c, ln, tt, seg_first, seg_last);
+        sgm_step_seg_t<NP, LPR, NOWRAP>(lp, delta2, p1x2, c, ln, tt, seg_first, seg_last);
         minp = seg_min_i32<LPR>(lane_min_row<NP>(ln));
         AR::template combine<NACC>(ab[j], acc);
         uint32_t key = 0x7fffffffu;
@@ -2162,7 +2199,7 @@ __global__ void fill_s16_kernel(int16_t* __restrict__ out, size_t os, size_t ofs
 }
 
 // sheared-strip schedule: enabled, and int32 element offsets cover a frame
-template <int NP, int NACC, typename AccT>
+template <int NP, int NACC, typename AccT, bool NW = false>
 void launch_final16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv,
                     const AccT* Av, size_t plane, int16_t* raw)
 {
@@ -2174,13 +2211,22 @@ void launch_final16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const 
     constexpr int RPW = 64 / LPR;
     const dim3 grid((H + RPW - 1) / RPW, n);
     if (e.uniq > 0)
-        hipLaunchKernelGGL((sgbm_final16_kernel<NPL, NACC, AccT, true, LPR>), grid, dim3(64), 0,
+        hipLaunchKernelGGL((sgbm_final16_kernel<NPL, NACC, AccT, true, LPR, NW>), grid, dim3(64), 0,
                            ctx->stream, Cv, Av, plane, H, W, e, raw, (uint32_t*)ctx->keys.ptr,
                            (int16_t*)ctx->dummy.ptr);
     else
-        hipLaunchKernelGGL((sgbm_final16_kernel<NPL, NACC, AccT, false, LPR>), grid, dim3(64), 0,
+        hipLaunchKernelGGL((sgbm_final16_kernel<NPL, NACC, AccT, false, LPR, NW>), grid, dim3(64), 0,
                            ctx->stream, Cv, Av, plane, H, W, e, raw, (uint32_t*)ctx->keys.ptr,
                            (int16_t*)ctx->dummy.ptr);
+}
+
+// Every cost C = P2 + (box sum of blockSize^2 BT costs, each <= 2*ftzero + 63),
+// every L <= C and delta = minLp + P2: when that bound stays <= 32767 nothing
+// wraps in int16 and the path kernels may use the NW recurrence (sgm_pair).
+static bool sgbm_no_wrap(const SgbmEff& e)
+{
+    const long bs = 2L * e.SW2 + 1;
+    return (long)e.P2 + bs * bs * (2L * e.ftzero + 63) + e.P2 <= 32767;
 }
 
 static bool use_strips(const mvsv_ctx* ctx, const SgbmEff& e, int H)
@@ -2188,7 +2234,7 @@ static bool use_strips(const mvsv_ctx* ctx, const SgbmEff& e, int H)
     return ctx->tri && (size_t)H * e.W1 * e.D < ((size_t)1 << 31);
 }
 
-template <int NP, typename AccT>
+template <int NP, typename AccT, bool NW>
 int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
                int npass)
 {
@@ -2226,7 +2272,7 @@ int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT*
         (void)hipMalloc(&stats, (size_t)grid.x * 64);
         (void)hipMemset(stats, 0, (size_t)grid.x * 64);
     }
-    hipLaunchKernelGGL((sgbm_tri_kernel<NP, AccT>), grid, dim3(TriCfg<NP>::kThreads), TL::kBytes,
+    hipLaunchKernelGGL((sgbm_tri_kernel<NP, AccT, NW>), grid, dim3(TriCfg<NP>::kThreads), TL::kBytes,
                        ctx->stream, Cv, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, npass, e.P1,
                        e.P2, (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips,
                        (int*)ctx->status.ptr, ctx->spin_limit, ctx->report_target, stats);
@@ -2264,7 +2310,7 @@ int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT*
 // ((1,-1) (0,-1) (-1,-1), MODE_HH) and the L->R lines each write their own
 // accumulator plane; the L->R lines run on a second stream beside the strip
 // kernel, and the final kernel (R->L + WTA) sums the planes.
-template <int NP, typename AccT>
+template <int NP, typename AccT, bool NW>
 int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, AccT* Av,
                      size_t plane, int16_t* raw)
 {
@@ -2287,7 +2333,7 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
         auto lines = [&]() {
             StageTimer tl(ctx, kStageLines, ls);
             dim3 grid((num_lines(1, 0, e.W1, H) + 15) / 16, n);
-            hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT>), grid, dim3(256), 0, ls, Cv,
+            hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT, NW>), grid, dim3(256), 0, ls, Cv,
                                acc_add(Av, (ptrdiff_t)npass * (ptrdiff_t)plane), dummy, H, e.W1,
                                e.D, 1, 0, e.P1, e.P2);
         };
@@ -2297,7 +2343,7 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
         if ((rc = check_hip(ctx, hipGetLastError(), "sgbm L->R lines"))) return rc;
         {
             StageTimer ts(ctx, kStageStrips);
-            if ((rc = launch_tri<NP, AccT>(ctx, n, H, e, Cv, Av, plane, npass))) return rc;
+            if ((rc = launch_tri<NP, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass))) return rc;
         }
         if (ctx->lines_aux != 1) lines();
         if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_join, ctx->aux), "join")) ||
@@ -2306,9 +2352,9 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
     }
     StageTimer tm(ctx, kStageFinal);
     if (npass == 2)
-        launch_final16<NP, 3, AccT>(ctx, n, H, W, e, Cv, Av, plane, raw);
+        launch_final16<NP, 3, AccT, NW>(ctx, n, H, W, e, Cv, Av, plane, raw);
     else
-        launch_final16<NP, 2, AccT>(ctx, n, H, W, e, Cv, Av, plane, raw);
+        launch_final16<NP, 2, AccT, NW>(ctx, n, H, W, e, Cv, Av, plane, raw);
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels (sheared strips)");
 }
 
@@ -2324,7 +2370,7 @@ int launch_paths16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t
     if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
     AccT* dummy = (AccT*)ctx->dummy.ptr;
     const size_t plane = (size_t)n * H * e.W1 * e.D;
-    if (use_strips(ctx, e, H)) return launch_paths_tri<NP, AccT>(ctx, n, H, W, e, Cv, Av, plane, raw);
+    if (use_strips(ctx, e, H)) return launch_paths_tri<NP, AccT, false>(ctx, n, H, W, e, Cv, Av, plane, raw);
     const int ndir = e.fullDP ? 7 : 4;
     for (int k = 0; k < ndir; k++) {
         int dx = e.fullDP ? dirs_hh[k][0] : dirs_sgbm[k][0];
@@ -2392,7 +2438,9 @@ int launch_paths16_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int
         if ((rc = ensure(ctx, ctx->dummy, 512 * 16 * 2 * NP, "sgbm dummy slots"))) return rc;
         if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
         const size_t plane = (size_t)n * H * e.W1 * e.D;
-        return launch_paths_tri<NP, nib2_t>(ctx, n, H, W, e, Cv, (nib2_t*)Av, plane, raw);
+        if (sgbm_no_wrap(e))
+            return launch_paths_tri<NP, nib2_t, true>(ctx, n, H, W, e, Cv, (nib2_t*)Av, plane, raw);
+        return launch_paths_tri<NP, nib2_t, false>(ctx, n, H, W, e, Cv, (nib2_t*)Av, plane, raw);
     }
     if (acc_is_u8(e)) return launch_paths16<NP, uint8_t>(ctx, n, H, W, e, Cv, (uint8_t*)Av, raw);
     return launch_paths16<NP, uint16_t>(ctx, n, H, W, e, Cv, (uint16_t*)Av, raw);
