@@ -21,6 +21,8 @@
 // W-ndisp-rofs) + k), so the border columns that validateDisparity sees
 // match OpenCV's sliding-sum implementation bit for bit.
 #include <algorithm>
+#include <cmath>
+#include <type_traits>
 
 #include "mvsv_device.hpp"
 #include "mvsv_internal.hpp"
@@ -243,6 +245,315 @@ __global__ __launch_bounds__(256) void bm_match_kernel(const uint8_t* __restrict
     if (cost) cost[((size_t)f * H + y) * W + ximg] = (int)minsad;
 }
 
+// ---------------------------------------------------------------------------
+// bm_match2_kernel: disparities on the lanes.  A 256-thread block stages the
+// prefiltered rows of a (64 / NR)-column x TY-row tile (plus the window halo)
+// in LDS.  The block's four waves form 4 / NR column groups of 16 output
+// columns; the NR waves of a group hold the disparity indices
+// kk = lane + 64 g (g = the wave's rank in its group) and walk down the tile's
+// rows together:
+//   * column sums of |L - R| over the window's rows per virtual column, kept in
+//     registers and slid down one row per step: one masked byte SAD
+//     (v_msad_u8) adds the new row, one subtracts the old.  Both views are
+//     staged as value + 1 (never 0, so the byte mask of v_msad_u8 selects one
+//     byte; differences are unchanged): the left view as one dword per pixel
+//     with the byte in lane (column & 3), read as wave-uniform b128 broadcasts,
+//     the right view as four byte-shifted dword copies, so lane kk reads the
+//     four right pixels of four consecutive columns with one ds_read_b32;
+//   * the window SAD of the 16 output columns by a sliding sum over the
+//     virtual columns, written to the group's [column][disparity] LDS slab
+//     (disparity indices >= numDisparities carry a +0x10000 offset per column
+//     sum, so they never win and never fail the uniqueness test);
+//   * the slab is re-read with 4 NR lanes per output column (each wave of the
+//     group takes 16 / NR of the columns), each lane scanning 16 disparity
+//     indices: argmin (ties -> smallest index, as OpenCV's ascending scan with
+//     '<') with keys (sad << 8 | index) and v_min3, DPP reductions; the
+//     uniqueness test masks the winner and its two neighbours in the slab and
+//     takes a second minimum; texture sums (column sums of |L - cap| slid the
+//     same way) and the parabola neighbours as bm_match_kernel.
+// Same virtual-column clamps and the same per-pixel decisions as
+// bm_match_kernel (which remains for blockSize > 21 or numDisparities > 128).
+// ---------------------------------------------------------------------------
+constexpr int kBm2Cols = 16;   // output columns per column group
+constexpr int kBm2Waves = 4;   // waves per block
+constexpr uint32_t kBm2Pad = 0x10000u;  // per-column offset of the unused disparity lanes
+
+struct Bm2Layout {
+    int NJ, NJP, NRW, NRC;
+    size_t copy, off_r, off_sad, off_tc, bytes;
+};
+
+__host__ __device__ inline Bm2Layout bm2_layout(int w2, int TY, int NR)
+{
+    Bm2Layout l;
+    l.NJ = kBm2Waves / NR * kBm2Cols + 2 * w2;
+    l.NJP = (l.NJ + 3) & ~3;
+    l.NRW = TY + 2 * w2;
+    l.NRC = (l.NJ + 64 * NR + 4 + 3) & ~3;  // right-view bytes per row
+    // four byte-shifted copies of the right view; copy stride = 32 mod 128
+    // bytes: a ds_read_b32 half-wave (32 lanes, banks = dword mod 32) reads 8
+    // consecutive dwords of each copy, at bank offsets 0 / 8 / 16 / 24
+    l.copy = (((size_t)l.NRW * l.NRC + 127) & ~(size_t)127) + 32;
+    l.off_r = (size_t)l.NRW * l.NJP * 4;
+    l.off_sad = l.off_r + 4 * l.copy;
+    // slabs of all groups: [column][NR * 64 + 4] -- the 16-byte pad puts the
+    // four columns of a ds_read_b128 lane group on different banks
+    l.off_tc = l.off_sad + (size_t)(kBm2Waves / NR) * kBm2Cols * (NR * 64 + 4) * 4;
+    l.bytes = l.off_tc + (size_t)kBm2Waves * 64 * 4;               // texture sums per wave
+    return l;
+}
+
+template <int NR, int W2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void bm_match2_kernel(
+    const uint8_t* __restrict__ Lf, const uint8_t* __restrict__ Rf, int W, int H, BmEff e,
+    int keep_border, int TY, int16_t* __restrict__ out, size_t os, size_t ofs,
+    int* __restrict__ cost)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int win = 2 * W2 + 1;
+    constexpr int BC = kBm2Waves / NR * kBm2Cols;  // output columns per block
+    constexpr int NC = kBm2Cols + 2 * W2;          // virtual columns of a column group
+    const int nd = e.ndisp;
+    const Bm2Layout lay = bm2_layout(W2, TY, NR);
+    const int NJ = lay.NJ, NJP = lay.NJP, NRW = lay.NRW, NRC = lay.NRC;
+    uint32_t* Lt = (uint32_t*)smem;         // [NRW][NJP] (L + 1) << 8 (c & 3)
+    uint8_t* Rp = smem + lay.off_r;         // copy 0: [NRW][NRC] bytes R + 1
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int cg = wv / NR, g = wv % NR;  // column group, disparity block of this wave
+    constexpr int SS = NR * 64 + 4;  // slab column stride (dwords)
+    uint32_t* sadx = (uint32_t*)(smem + lay.off_sad) + (size_t)cg * kBm2Cols * SS;
+    int* tcb = (int*)(smem + lay.off_tc) + wv * 64;
+    const int f = blockIdx.z;
+    const int xl0 = blockIdx.x * BC;
+    const int yr0 = e.ymin + blockIdx.y * TY;
+    const int lofs = e.lofs, rofs = e.rofs;
+    const uint8_t* Lfr = Lf + (size_t)f * W * H;
+    const uint8_t* Rfr = Rf + (size_t)f * W * H;
+    const int jmin = xl0 - W2;
+    auto clampL = [&](int j) { return lofs + clampi(j, -lofs, W - 1 - lofs); };
+    auto clampR = [&](int j) { return clampi(j, -rofs, W - nd - rofs); };
+    const int rbase = clampR(jmin);
+
+    // staging (no per-element division: the (row, column) pair steps by 256)
+    {
+        int r = tid / NJ, c = tid - r * NJ;
+        const int dr = 256 / NJ, dc = 256 - dr * NJ;
+        for (; r < NRW;) {
+            const int yy = clampi(yr0 - W2 + r, 0, H - 1);
+            Lt[r * NJP + c] = (uint32_t)(Lfr[(size_t)yy * W + clampL(jmin + c)] + 1) << (8 * (c & 3));
+            c += dc;
+            r += dr;
+            if (c >= NJ) {
+                c -= NJ;
+                r++;
+            }
+        }
+    }
+    {
+        int r = tid / NRC, c = tid - r * NRC;
+        const int dr = 256 / NRC, dc = 256 - dr * NRC;
+        for (; r < NRW;) {
+            const int yy = clampi(yr0 - W2 + r, 0, H - 1);
+            Rp[r * NRC + c] = (uint8_t)(Rfr[(size_t)yy * W + min(rofs + rbase + c, W - 1)] + 1);
+            c += dc;
+            r += dr;
+            if (c >= NRC) {
+                c -= NRC;
+                r++;
+            }
+        }
+    }
+    __syncthreads();
+    {  // copies 1..3: dword i of copy s = bytes [4 i + s, 4 i + s + 4) of copy 0
+        const uint32_t* p0 = (const uint32_t*)Rp;
+        const int nd4 = NRW * NRC / 4;
+        for (int i = tid; i < 3 * nd4; i += 256) {
+            const int s = i / nd4 + 1, k = i - (s - 1) * nd4;
+            ((uint32_t*)(Rp + s * lay.copy))[k] = __builtin_amdgcn_alignbyte(p0[k + 1], p0[k], s);
+        }
+    }
+
+    const int c0 = cg * kBm2Cols;  // the group's first virtual column in the tile
+    const int rows = min(TY, e.ymax - yr0);
+    // right-tile column of virtual column v: rcol(v) = clampR(jmin + c0 + v) - rbase
+    // (wave-uniform).  Groups without a clamp inside their NC columns address
+    // it as rcol(0) + v through the shifted copies; the others read rcol(v)
+    // byte by byte.
+    const int cr0 = clampR(jmin + c0) - rbase;
+    const bool lin = clampR(jmin + c0 + NC - 1) - rbase == cr0 + NC - 1;
+    const int kl = lane + 64 * g;  // this lane's disparity index in the column-sum phase
+    const uint32_t pad = kl < nd ? 0u : kBm2Pad;
+    const int rb = cr0 + kl;  // lin: right byte of virtual column v = rb + v
+    const uint32_t* Rq = (const uint32_t*)(Rp + (rb & 3) * lay.copy) + (rb >> 2);
+    const uint32_t capsh = (uint32_t)(e.cap + 1) << (8 * ((c0 + lane) & 3));
+    __syncthreads();
+
+    // argmin phase: output column qx of the group (LPC lanes each), sub-lane h
+    // scans the disparity indices [16 h, 16 h + 16)
+    constexpr int LPC = 4 * NR, CPW = kBm2Cols / NR;
+    const int qx = g * CPW + lane / LPC, h = lane % LPC;
+    const int xl = xl0 + c0 + qx;
+    const int ximg = lofs + xl;
+    const bool active = xl < e.ncol;
+    const bool border = !keep_border && (ximg < e.xmin || ximg >= e.xmax);
+
+    uint32_t cs[NC];
+    uint32_t tc = 0;  // texture column sum of virtual column `lane` (lanes < NC)
+    auto colsums = [&](auto LIN, int t) {
+        constexpr bool kLin = decltype(LIN)::value;
+        // |L - R| of row r, virtual column v, added to acc
+        auto absd = [&](int r, int v, uint32_t lw, uint32_t acc) -> uint32_t {
+            if constexpr (kLin) {
+                return __builtin_amdgcn_msad_u8(Rq[r * (NRC / 4) + (v >> 2)], lw, acc);
+            } else {
+                // opaque row base: keeps the compiler from hoisting one
+                // address register per column out of the row loop
+                uint32_t rowo = (uint32_t)(lay.off_r + kl + r * NRC);  // byte offset in smem
+                asm volatile("" : "+v"(rowo));
+                const uint32_t rbyte = smem[rowo + (uint32_t)(clampR(jmin + c0 + v) - rbase)];
+                return __builtin_amdgcn_msad_u8(rbyte << (8 * (v & 3)), lw, acc);
+            }
+        };
+        if (t == 0) {
+#pragma unroll
+            for (int v = 0; v < NC; v++) cs[v] = pad;
+#pragma unroll 1
+            for (int r = 0; r < win; r++) {
+                const uint32_t* Lr = Lt + r * NJP + c0;
+#pragma unroll
+                for (int v = 0; v < NC; v++) cs[v] = absd(r, v, Lr[v], cs[v]);
+                tc = __builtin_amdgcn_sad_u8(Lr[lane], capsh, tc);
+            }
+        } else {
+            const int rn = t + win - 1, ro = t - 1;
+            const uint32_t* Ln = Lt + rn * NJP + c0;
+            const uint32_t* Lo = Lt + ro * NJP + c0;
+            tc = __builtin_amdgcn_sad_u8(Ln[lane], capsh, tc) - __builtin_amdgcn_sad_u8(Lo[lane], capsh, 0u);
+#pragma unroll
+            for (int v = 0; v < NC; v++) {
+                const uint32_t add = absd(rn, v, Ln[v], cs[v]);
+                cs[v] = add - absd(ro, v, Lo[v], 0u);
+                // bound the LDS loads the scheduler hoists (registers)
+                if ((v & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    };
+    auto group_sync = [&]() {
+        if constexpr (NR == 1) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+            __syncthreads();
+        }
+    };
+    auto wave_sync = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (int t = 0; t < rows; t++) {
+        if (lin)
+            colsums(std::integral_constant<bool, true>(), t);
+        else
+            colsums(std::integral_constant<bool, false>(), t);
+        // window SADs of the group's 16 output columns -> slab [column][disparity]
+        {
+            uint32_t sum = 0;
+#pragma unroll
+            for (int v = 0; v < win; v++) sum += cs[v];
+            sadx[g * 64 + lane] = sum;
+#pragma unroll
+            for (int x = 1; x < kBm2Cols; x++) {
+                sum += cs[x + win - 1];
+                sum -= cs[x - 1];
+                sadx[x * SS + g * 64 + lane] = sum;
+            }
+        }
+        tcb[lane] = (int)tc;
+        group_sync();
+        uint32_t* srow = sadx + qx * SS;
+        const int k0 = h * 16;
+        // argmin over this lane's 16 slab entries, keys (sad << 8) | index
+        uint32_t best;
+        {
+            uint32_t key[16];
+#pragma unroll
+            for (int i = 0; i < 16; i += 4) {
+                const uint4 w = *(const uint4*)(srow + k0 + i);
+                key[i] = (w.x << 8) | (uint32_t)i;
+                key[i + 1] = (w.y << 8) | (uint32_t)(i + 1);
+                key[i + 2] = (w.z << 8) | (uint32_t)(i + 2);
+                key[i + 3] = (w.w << 8) | (uint32_t)(i + 3);
+            }
+            best = min(key[0], key[1]);
+#pragma unroll
+            for (int i = 2; i < 16; i += 2) best = min(min(best, key[i]), key[i + 1]);
+            best |= (uint32_t)k0;
+        }
+        best = min(best, (uint32_t)__builtin_amdgcn_mov_dpp((int)best, 0xB1, 0xf, 0xf, false));
+        best = min(best, (uint32_t)__builtin_amdgcn_mov_dpp((int)best, 0x4E, 0xf, 0xf, false));
+        if constexpr (NR == 2)  // row_half_mirror: quad 0 <-> quad 1 of each 8 lanes
+            best = min(best, (uint32_t)__builtin_amdgcn_mov_dpp((int)best, 0x141, 0xf, 0xf, false));
+        const int mind = (int)(best & 0xff);
+        const uint32_t minsad = best >> 8;
+        // parabola neighbours (read before the uniqueness pass masks them)
+        const int pp = (int)srow[min(mind + 1, 64 * NR - 1)];
+        const int nn = (int)srow[max(mind - 1, 0)];
+        bool bad = false;
+        if (e.uniq > 0) {
+            const uint32_t ms = minsad;
+            const uint32_t thresh = ms + (uint32_t)((int)ms * e.uniq / 100);
+            wave_sync();  // every lane of the column has read the slab row
+            if (h == 0) {
+                srow[mind] = 0xffffffffu;
+                if (mind > 0) srow[mind - 1] = 0xffffffffu;
+                if (mind + 1 < 64 * NR) srow[mind + 1] = 0xffffffffu;
+            }
+            wave_sync();
+            uint32_t m2 = 0xffffffffu;
+#pragma unroll
+            for (int i = 0; i < 16; i += 4) {
+                const uint4 w = *(const uint4*)(srow + k0 + i);
+                m2 = min(min(m2, w.x), w.y);
+                m2 = min(min(m2, w.z), w.w);
+            }
+            m2 = min(m2, (uint32_t)__builtin_amdgcn_mov_dpp((int)m2, 0xB1, 0xf, 0xf, false));
+            m2 = min(m2, (uint32_t)__builtin_amdgcn_mov_dpp((int)m2, 0x4E, 0xf, 0xf, false));
+            if constexpr (NR == 2)
+                m2 = min(m2, (uint32_t)__builtin_amdgcn_mov_dpp((int)m2, 0x141, 0xf, 0xf, false));
+            bad = m2 <= thresh;
+        }
+        int tsum = 0;
+#pragma unroll
+        for (int qq = 0; qq < win; qq++) tsum += tcb[qx + qq];
+        const int y = yr0 + t;
+        if (h == 0 && active) {
+            int16_t* op = out + f * ofs + (size_t)y * os + ximg;
+            int16_t res;
+            bool computed = false;
+            if (border || tsum < e.tex || bad) {
+                res = (int16_t)e.filtered;
+            } else {
+                const int v1 = nd - mind - 1 + e.mindisp;
+                int val;
+                if (0 < mind && mind < nd - 1) {
+                    const int d = pp + nn - 2 * (int)minsad + abs(pp - nn);
+                    val = (v1 * 256 + (d != 0 ? (pp - nn) * 256 / d : 0) + 15) >> 4;
+                } else {
+                    val = (v1 * 256 + 15) >> 4;
+                }
+                res = (int16_t)val;
+                computed = true;
+            }
+            *op = res;
+            if (cost && computed) cost[((size_t)f * H + y) * W + ximg] = (int)minsad;
+        }
+        group_sync();
+    }
+}
+
 // [OpenCV] validateDisparity, one block per valid row: the right-view winner
 // per x2 is the smallest cost, ties -> the smallest x (first in the scan).
 __global__ __launch_bounds__(256) void bm_validate_kernel(int16_t* __restrict__ out, size_t os,
@@ -301,6 +612,9 @@ __global__ void bm_roi_kernel(int16_t* __restrict__ out, size_t os, size_t ofs, 
 
 }  // namespace
 
+static int bm_finish(mvsv_ctx* ctx, int n, int W, int H, const BmEff& e, int16_t* out, size_t os,
+                     size_t ofs, int* cost);
+
 int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, const uint8_t* R,
               size_t rs, size_t rfs, int W, int H, const BmEff& e, int16_t* out, size_t os,
               size_t ofs)
@@ -341,6 +655,61 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
         cost = (int*)ctx->bm_cost.ptr;
     }
     const int win = 2 * e.wsz2 + 1;
+    // disparities on the lanes (bm_match2_kernel) for blockSize <= 21 and
+    // numDisparities <= 128; the 16x16-tile kernel otherwise
+    if (ctx->bm2 && e.wsz2 >= 2 && e.wsz2 <= 10 && e.ndisp <= 128) {
+        const int NR = e.ndisp > 64 ? 2 : 1;
+        const int BC = kBm2Waves / NR * kBm2Cols;
+        const int gx = (e.ncol + BC - 1) / BC, nrows = e.ymax - e.ymin;
+        // tile height: rounds of resident blocks x (rows + start-up of the
+        // window, ~win / 4 + 1 rows), with a penalty for fewer than four
+        // resident blocks per CU (the kernel hides LDS latency with waves);
+        // fitted to configs 1 / 2 at batch 1 and 8 (tools/bm_time.py sweep)
+        int TY = ctx->bm_ty;
+        if (TY <= 0) {
+            double best = 1e30;
+            for (int ty = 4; ty <= 64; ty += 4) {
+                const size_t bytes = bm2_layout(e.wsz2, ty, NR).bytes;
+                if (bytes > 160 * 1024) break;
+                const long long k = std::min<long long>(4, (160 * 1024) / (long long)bytes);
+                const long long blocks = (long long)gx * ((nrows + ty - 1) / ty) * n;
+                const long long rounds = (blocks + ctx->cus * k - 1) / (ctx->cus * k);
+                const double c = rounds * (ty + win * 0.25 + 1) * std::pow(4.0 / k, 0.6);
+                if (c < best - 1e-9) {
+                    best = c;
+                    TY = ty;
+                }
+            }
+        }
+        const Bm2Layout l2 = bm2_layout(e.wsz2, TY, NR);
+        if (l2.bytes > 160 * 1024)
+            return set_error(ctx, MVSV_E_INVALID_ARG, "BM tile height too large for LDS");
+        typedef void (*Bm2Fn)(const uint8_t*, const uint8_t*, int, int, BmEff, int, int, int16_t*,
+                              size_t, size_t, int*);
+        static const Bm2Fn fns[2][9] = {
+            {bm_match2_kernel<1, 2>, bm_match2_kernel<1, 3>, bm_match2_kernel<1, 4>,
+             bm_match2_kernel<1, 5>, bm_match2_kernel<1, 6>, bm_match2_kernel<1, 7>,
+             bm_match2_kernel<1, 8>, bm_match2_kernel<1, 9>, bm_match2_kernel<1, 10>},
+            {bm_match2_kernel<2, 2>, bm_match2_kernel<2, 3>, bm_match2_kernel<2, 4>,
+             bm_match2_kernel<2, 5>, bm_match2_kernel<2, 6>, bm_match2_kernel<2, 7>,
+             bm_match2_kernel<2, 8>, bm_match2_kernel<2, 9>, bm_match2_kernel<2, 10>}};
+        const Bm2Fn kern = fns[NR - 1][e.wsz2 - 2];
+        if (l2.bytes > 65536 &&
+            (rc = check_hip(ctx, hipFuncSetAttribute((const void*)kern,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)l2.bytes),
+                            "bm LDS attribute")))
+            return rc;
+        dim3 grid2(gx,
+                   (e.ymax - e.ymin + TY - 1) / TY, n);
+        {
+            StageTimer tm(ctx, kStageBm);
+            hipLaunchKernelGGL(kern, grid2, dim3(256), l2.bytes, s, Lf, Rf, W, H, e, validate ? 1 : 0, TY,
+                               out, os, ofs, cost);
+        }
+        if ((rc = check_hip(ctx, hipGetLastError(), "bm match"))) return rc;
+        return bm_finish(ctx, n, W, H, e, out, os, ofs, cost);
+    }
     const bool small = (long long)win * win * 2 * e.cap <= 65535;
     BmLayout lay = bm_layout(e.ndisp, e.wsz2, small ? 2 : 4);
     if (lay.bytes > 160 * 1024)
@@ -363,6 +732,16 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
         hipLaunchKernelGGL(bm_match_kernel<uint32_t>, grid, dim3(256), lay.bytes, s, Lf, Rf, W, H,
                            e, validate ? 1 : 0, out, os, ofs, cost);
     if ((rc = check_hip(ctx, hipGetLastError(), "bm match"))) return rc;
+    return bm_finish(ctx, n, W, H, e, out, os, ofs, cost);
+}
+
+// validateDisparity + ROI + speckle after either match kernel
+static int bm_finish(mvsv_ctx* ctx, int n, int W, int H, const BmEff& e, int16_t* out, size_t os,
+                     size_t ofs, int* cost)
+{
+    hipStream_t s = ctx->stream;
+    int rc;
+    const bool validate = e.disp12 >= 0;
     if (validate) {
         size_t lds = (size_t)W * 8 + (size_t)W * 2;
         hipLaunchKernelGGL(bm_validate_kernel, dim3(e.ymax - e.ymin, n), dim3(256), lds, s, out, os,

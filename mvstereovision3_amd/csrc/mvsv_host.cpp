@@ -260,8 +260,14 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
         if (std::strstr(v, "cost-lds")) c->cost2 = 0;
         if (std::strstr(v, "path-wave")) c->path16 = 0;
         if (std::strstr(v, "path-lines")) c->tri = 0;
+        if (std::strstr(v, "bm-tile")) c->bm2 = 0;
     }
     if (const char* v = std::getenv("MVSV_COST_TY")) c->cost_ty = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("MVSV_BM_TY")) c->bm_ty = std::max(0, std::min(128, std::atoi(v)));
+    if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess) {
+        (void)hipGetLastError();
+        c->cus = 256;
+    }
     if (const char* v = std::getenv("MVSV_LINES_AUX")) c->lines_aux = std::max(0, std::min(2, std::atoi(v)));
     *out = c;
     return MVSV_OK;

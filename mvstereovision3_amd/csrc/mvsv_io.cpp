@@ -171,6 +171,8 @@ int mvsv_load_bm_yaml(const char* path, mvsv_bm_params* p)
 // ---------------------------------------------------------------------------
 // Synthetic rectified pair.
 // ---------------------------------------------------------------------------
+}  // extern "C"
+
 namespace {
 struct Pcg32 {
     uint64_t state;
@@ -186,6 +188,8 @@ struct Pcg32 {
     }
 };
 }  // namespace
+
+extern "C" {
 
 int mvsv_synth_pair(uint32_t seed, int W, int H, int minD, int D, uint8_t* Lout, uint8_t* Rout)
 {
@@ -372,6 +376,8 @@ int mvsv_init_undistort_rectify_map(const double* K, const double* dist, int ndi
 // which would end past column 71 (continuation indent 7), doubles as "%.16e"
 // and floats as "%.8e" unless integral ("%d."), ".Nan" / ".Inf" / "-.Inf".
 // ---------------------------------------------------------------------------
+}  // extern "C"
+
 namespace {
 
 constexpr int kYmlWrap = 71;
@@ -523,6 +529,8 @@ void empty_mat(mvsv_mat* m)
 
 }  // namespace
 
+extern "C" {
+
 int mvsv_read_matrix_yaml(const char* path, const char* key, mvsv_mat* out)
 {
     if (!key || !out) return MVSV_E_INVALID_ARG;
@@ -621,6 +629,8 @@ int mvsv_save_extrinsic(const char* path, const mvsv_extrinsics* in)
 // Double-precision restatement: Rodrigues without OpenCV's SVD
 // re-orthogonalisation of R, so results may differ in the last bits.
 // ---------------------------------------------------------------------------
+}  // extern "C"
+
 namespace {
 
 void mat3_mul(const double* A, const double* B, double* C, bool bt = false)
@@ -761,6 +771,8 @@ mvsv_rect rect_and(mvsv_rect a, mvsv_rect b)  // cv::Rect & (as x0,y0,x1,y1)
 }
 
 }  // namespace
+
+extern "C" {
 
 int mvsv_stereo_rectify(const double* K1, const double* D1, int nd1, const double* K2,
                         const double* D2, int nd2, int W, int H, const double* Rm,

@@ -1828,9 +1828,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     const bool lane_rule = !e.fullDP && !(e.variant & MVSV_VARIANT_WTA_MIN_D);
     const size_t frame = (size_t)H * W1 * D;
     const int d0 = rl * 2 * NP;
-    const size_t off = f * frame + ((size_t)y * W1 + (W1 - 1)) * D + d0;
-    const int16_t* cp = C + off;
-    const AccT* sp = acc_add(A, (ptrdiff_t)off);
     uint16_t* ms = srow + row * DR;
     uint32_t lp[NP];
 #pragma unroll
