@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
     constexpr int NC = kBm2Cols + 2 * W2;          // virtual columns of a column group
     const int nd = e.ndisp;
     const Bm2Layout lay = bm2_layout(W2, TY, NR);
-    const int NJ = lay.NJ, NJP = lay.NJP, NRW = lay.NRW, NRC = lay.NRC;
+    const int NJP = lay.NJP, NRW = lay.NRW, NRC = lay.NRC;
     uint32_t* Lt = (uint32_t*)smem;         // [NRW][NJP] (L + 1) << 8 (c & 3)
     uint8_t* Rp = smem + lay.off_r;         // copy 0: [NRW][NRC] bytes R + 1
     const int tid = threadIdx.x, lane = tid & 63;
@@ -331,46 +331,81 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
     const uint8_t* Lfr = Lf + (size_t)f * W * H;
     const uint8_t* Rfr = Rf + (size_t)f * W * H;
     const int jmin = xl0 - W2;
-    auto clampL = [&](int j) { return lofs + clampi(j, -lofs, W - 1 - lofs); };
+    // left tile column c <- image column clamp(lofs + jmin + c, 0, W - 1)
+    // (OpenCV's left clamp); right: clampR below, the tile starting at rbase
     auto clampR = [&](int j) { return clampi(j, -rofs, W - nd - rofs); };
     const int rbase = clampR(jmin);
 
-    // staging (no per-element division: the (row, column) pair steps by 256)
+    // staging: dword loads (two aligned dwords funnel-shifted per four bytes;
+    // the prefilter buffers carry 64 bytes of tail padding), byte loads only
+    // where a clamp falls inside the four / eight bytes.  One item = four left
+    // pixels (-> four shifted dwords, one b128 store) or four right-view
+    // dwords (bytes [4 i, 4 i + 8) of the row -> dword i of the four copies).
+    auto load4 = [](const uint8_t* p) -> uint32_t {
+        const uintptr_t a = (uintptr_t)p;
+        const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+        return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+    };
     {
-        int r = tid / NJ, c = tid - r * NJ;
-        const int dr = 256 / NJ, dc = 256 - dr * NJ;
-        for (; r < NRW;) {
+        const int NJ4 = NJP / 4;
+        const int items = NRW * NJ4;
+        int r = tid / NJ4, q = tid - r * NJ4;
+        const int dr = 256 / NJ4, dq = 256 - dr * NJ4;
+        for (int it = tid; it < items; it += 256) {
             const int yy = clampi(yr0 - W2 + r, 0, H - 1);
-            Lt[r * NJP + c] = (uint32_t)(Lfr[(size_t)yy * W + clampL(jmin + c)] + 1) << (8 * (c & 3));
-            c += dc;
+            const uint8_t* row = Lfr + (size_t)yy * W;
+            const int x0 = lofs + jmin + 4 * q;
+            uint32_t w;
+            if (x0 >= 0 && x0 + 3 <= W - 1) {
+                w = load4(row + x0);
+            } else {
+                w = 0;
+                for (int b = 0; b < 4; b++) w |= (uint32_t)row[clampi(x0 + b, 0, W - 1)] << (8 * b);
+            }
+            w += 0x01010101u;  // prefiltered values <= 126: no carries
+            *(uint4*)(Lt + r * NJP + 4 * q) =
+                make_uint4(w & 0xffu, w & 0xff00u, w & 0xff0000u, w & 0xff000000u);
+            q += dq;
             r += dr;
-            if (c >= NJ) {
-                c -= NJ;
+            if (q >= NJ4) {
+                q -= NJ4;
                 r++;
             }
         }
     }
     {
-        int r = tid / NRC, c = tid - r * NRC;
-        const int dr = 256 / NRC, dc = 256 - dr * NRC;
-        for (; r < NRW;) {
+        const int NR4 = NRC / 4;
+        const int items = NRW * NR4;
+        int r = tid / NR4, i = tid - r * NR4;
+        const int dr = 256 / NR4, di = 256 - dr * NR4;
+        for (int it = tid; it < items; it += 256) {
             const int yy = clampi(yr0 - W2 + r, 0, H - 1);
-            Rp[r * NRC + c] = (uint8_t)(Rfr[(size_t)yy * W + min(rofs + rbase + c, W - 1)] + 1);
-            c += dc;
+            const uint8_t* row = Rfr + (size_t)yy * W;
+            const int x0 = rofs + rbase + 4 * i;  // >= 0
+            uint32_t lo, hi;
+            if (x0 + 7 <= W - 1) {
+                lo = load4(row + x0);
+                hi = load4(row + x0 + 4);
+            } else {
+                lo = hi = 0;
+                for (int b = 0; b < 4; b++) {
+                    lo |= (uint32_t)row[min(x0 + b, W - 1)] << (8 * b);
+                    hi |= (uint32_t)row[min(x0 + 4 + b, W - 1)] << (8 * b);
+                }
+            }
+            lo += 0x01010101u;
+            hi += 0x01010101u;
+            uint32_t* d = (uint32_t*)Rp + r * NR4 + i;
+            d[0] = lo;
+            d[lay.copy / 4] = __builtin_amdgcn_alignbyte(hi, lo, 1);
+            d[2 * (lay.copy / 4)] = __builtin_amdgcn_alignbyte(hi, lo, 2);
+            d[3 * (lay.copy / 4)] = __builtin_amdgcn_alignbyte(hi, lo, 3);
+            i += di;
             r += dr;
-            if (c >= NRC) {
-                c -= NRC;
+            if (i >= NR4) {
+                i -= NR4;
                 r++;
             }
-        }
-    }
-    __syncthreads();
-    {  // copies 1..3: dword i of copy s = bytes [4 i + s, 4 i + s + 4) of copy 0
-        const uint32_t* p0 = (const uint32_t*)Rp;
-        const int nd4 = NRW * NRC / 4;
-        for (int i = tid; i < 3 * nd4; i += 256) {
-            const int s = i / nd4 + 1, k = i - (s - 1) * nd4;
-            ((uint32_t*)(Rp + s * lay.copy))[k] = __builtin_amdgcn_alignbyte(p0[k + 1], p0[k], s);
         }
     }
 
@@ -400,7 +435,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
 
     uint32_t cs[NC];
     uint32_t tc = 0;  // texture column sum of virtual column `lane` (lanes < NC)
-    auto colsums = [&](auto LIN, int t) {
+    auto colsums = [&](auto LIN, auto INIT, int t) {
         constexpr bool kLin = decltype(LIN)::value;
         // |L - R| of row r, virtual column v, added to acc
         auto absd = [&](int r, int v, uint32_t lw, uint32_t acc) -> uint32_t {
@@ -415,7 +450,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
                 return __builtin_amdgcn_msad_u8(rbyte << (8 * (v & 3)), lw, acc);
             }
         };
-        if (t == 0) {
+        if constexpr (decltype(INIT)::value) {
 #pragma unroll
             for (int v = 0; v < NC; v++) cs[v] = pad;
 #pragma unroll 1
@@ -453,11 +488,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    for (int t = 0; t < rows; t++) {
-        if (lin)
-            colsums(std::integral_constant<bool, true>(), t);
-        else
-            colsums(std::integral_constant<bool, false>(), t);
+    // one row's window SADs, argmin, tests and output
+    auto row_out = [&](int t) {
         // window SADs of the group's 16 output columns -> slab [column][disparity]
         {
             uint32_t sum = 0;
@@ -551,7 +583,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
             if (cost && computed) cost[((size_t)f * H + y) * W + ximg] = (int)minsad;
         }
         group_sync();
-    }
+    };
+    // the whole row walk per addressing variant (no register copies between
+    // variants at the loop back edge); row 0 builds the column sums
+    auto walk = [&](auto LIN) {
+        colsums(LIN, std::true_type(), 0);
+        row_out(0);
+        for (int t = 1; t < rows; t++) {
+            colsums(LIN, std::false_type(), t);
+            row_out(t);
+        }
+    };
+    if (lin)
+        walk(std::true_type());
+    else
+        walk(std::false_type());
 }
 
 // [OpenCV] validateDisparity, one block per valid row: the right-view winner
@@ -627,8 +673,9 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
     if (e.lofs >= W || e.rofs >= W || e.width1 < 1) return MVSV_OK;
     if (e.xmax - e.xmin <= 0 || e.ymax - e.ymin <= 0 || e.ncol <= 0) return MVSV_OK;
     const size_t plane = (size_t)W * H;
-    if ((rc = ensure(ctx, ctx->bm_lf, (size_t)n * plane, "bm left prefilter"))) return rc;
-    if ((rc = ensure(ctx, ctx->bm_rf, (size_t)n * plane, "bm right prefilter"))) return rc;
+    // + 64: the match kernel's staging reads whole aligned dwords past a row end
+    if ((rc = ensure(ctx, ctx->bm_lf, (size_t)n * plane + 64, "bm left prefilter"))) return rc;
+    if ((rc = ensure(ctx, ctx->bm_rf, (size_t)n * plane + 64, "bm right prefilter"))) return rc;
     uint8_t* Lf = (uint8_t*)ctx->bm_lf.ptr;
     uint8_t* Rf = (uint8_t*)ctx->bm_rf.ptr;
     if (e.prefilter_type == MVSV_PREFILTER_XSOBEL) {
@@ -661,29 +708,6 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
         const int NR = e.ndisp > 64 ? 2 : 1;
         const int BC = kBm2Waves / NR * kBm2Cols;
         const int gx = (e.ncol + BC - 1) / BC, nrows = e.ymax - e.ymin;
-        // tile height: rounds of resident blocks x (rows + start-up of the
-        // window, ~win / 4 + 1 rows), with a penalty for fewer than four
-        // resident blocks per CU (the kernel hides LDS latency with waves);
-        // fitted to configs 1 / 2 at batch 1 and 8 (tools/bm_time.py sweep)
-        int TY = ctx->bm_ty;
-        if (TY <= 0) {
-            double best = 1e30;
-            for (int ty = 4; ty <= 64; ty += 4) {
-                const size_t bytes = bm2_layout(e.wsz2, ty, NR).bytes;
-                if (bytes > 160 * 1024) break;
-                const long long k = std::min<long long>(4, (160 * 1024) / (long long)bytes);
-                const long long blocks = (long long)gx * ((nrows + ty - 1) / ty) * n;
-                const long long rounds = (blocks + ctx->cus * k - 1) / (ctx->cus * k);
-                const double c = rounds * (ty + win * 0.25 + 1) * std::pow(4.0 / k, 0.6);
-                if (c < best - 1e-9) {
-                    best = c;
-                    TY = ty;
-                }
-            }
-        }
-        const Bm2Layout l2 = bm2_layout(e.wsz2, TY, NR);
-        if (l2.bytes > 160 * 1024)
-            return set_error(ctx, MVSV_E_INVALID_ARG, "BM tile height too large for LDS");
         typedef void (*Bm2Fn)(const uint8_t*, const uint8_t*, int, int, BmEff, int, int, int16_t*,
                               size_t, size_t, int*);
         static const Bm2Fn fns[2][9] = {
@@ -694,6 +718,42 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
              bm_match2_kernel<2, 5>, bm_match2_kernel<2, 6>, bm_match2_kernel<2, 7>,
              bm_match2_kernel<2, 8>, bm_match2_kernel<2, 9>, bm_match2_kernel<2, 10>}};
         const Bm2Fn kern = fns[NR - 1][e.wsz2 - 2];
+        // resident blocks per CU from the kernel's registers (4 waves per
+        // block, one per SIMD; 512 VGPRs per SIMD lane)
+        static int vgpr_blocks_of[2][9];  // 0 = not queried yet (same value on every gfx950)
+        int vgpr_blocks = vgpr_blocks_of[NR - 1][e.wsz2 - 2];
+        if (vgpr_blocks <= 0) {
+            hipFuncAttributes fa;
+            vgpr_blocks = 4;
+            if (hipFuncGetAttributes(&fa, (const void*)kern) == hipSuccess && fa.numRegs > 0)
+                vgpr_blocks = std::max(1, std::min(8, 512 / ((fa.numRegs + 7) & ~7)));
+            else
+                (void)hipGetLastError();
+            vgpr_blocks_of[NR - 1][e.wsz2 - 2] = vgpr_blocks;
+        }
+        // tile height: rounds of resident blocks x (rows + start-up of the
+        // window, ~win / 4 + 1 rows), with a penalty for fewer than four
+        // resident blocks per CU (the kernel hides LDS latency with waves);
+        // fitted to configs 1 / 2 at batch 1 and 8 (tools/bm_time.py sweep)
+        int TY = ctx->bm_ty;
+        if (TY <= 0) {
+            double best = 1e30;
+            for (int ty = 4; ty <= 64; ty += 4) {
+                const size_t bytes = bm2_layout(e.wsz2, ty, NR).bytes;
+                if (bytes > 160 * 1024) break;
+                const long long k = std::min<long long>(vgpr_blocks, (160 * 1024) / (long long)bytes);
+                const long long blocks = (long long)gx * ((nrows + ty - 1) / ty) * n;
+                const long long rounds = (blocks + ctx->cus * k - 1) / (ctx->cus * k);
+                const double c = rounds * (ty + win * 0.25 + 1) * std::pow(4.0 / std::min<long long>(k, 4), 0.6);
+                if (c < best - 1e-9) {
+                    best = c;
+                    TY = ty;
+                }
+            }
+        }
+        const Bm2Layout l2 = bm2_layout(e.wsz2, TY, NR);
+        if (l2.bytes > 160 * 1024)
+            return set_error(ctx, MVSV_E_INVALID_ARG, "BM tile height too large for LDS");
         if (l2.bytes > 65536 &&
             (rc = check_hip(ctx, hipFuncSetAttribute((const void*)kern,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
