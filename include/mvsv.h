@@ -92,7 +92,10 @@ enum {
     /* polls a strip-boundary wait of the SGBM path kernel makes before it gives
      * up (default 1 << 20, ~1 s); 0 gives up at the first poll that finds the
      * producer's data not yet written (fault injection for tests) */
-    MVSV_OPT_STRIP_SPIN_LIMIT = 1
+    MVSV_OPT_STRIP_SPIN_LIMIT = 1,
+    /* rows per block of the StereoBM disparities-on-lanes kernel (0 = chosen
+     * per launch from the shape; 1..128 forces it -- tests, A/B runs) */
+    MVSV_OPT_BM_TILE_ROWS = 2
 };
 
 /* StereoSGBM modes (cv::StereoSGBM::MODE_SGBM / MODE_HH). */

@@ -398,6 +398,10 @@ int mvsv_set_option(mvsv_ctx* ctx, int option, long long value)
             return set_error(ctx, MVSV_E_INVALID_ARG, "spin limit must be 0..2^32-1");
         ctx->spin_limit = (unsigned)value;
         return MVSV_OK;
+    case MVSV_OPT_BM_TILE_ROWS:
+        if (value < 0 || value > 128) return set_error(ctx, MVSV_E_INVALID_ARG, "BM tile rows must be 0..128");
+        ctx->bm_ty = (int)value;
+        return MVSV_OK;
     default:
         return set_error(ctx, MVSV_E_INVALID_ARG, "unknown option");
     }
