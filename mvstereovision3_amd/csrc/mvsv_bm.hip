@@ -280,7 +280,7 @@ constexpr uint32_t kBm2Pad = 0x10000u;  // per-column offset of the unused dispa
 
 struct Bm2Layout {
     int NJ, NJP, NRW, NRC;
-    size_t copy, off_r, off_sad, off_tc, bytes;
+    size_t copy, off_r, off_sad, off_tc, off_rec, bytes;
 };
 
 __host__ __device__ inline Bm2Layout bm2_layout(int w2, int TY, int NR)
@@ -299,7 +299,8 @@ __host__ __device__ inline Bm2Layout bm2_layout(int w2, int TY, int NR)
     // slabs of all groups: [column][NR * 64 + 4] -- the 16-byte pad puts the
     // four columns of a ds_read_b128 lane group on different banks
     l.off_tc = l.off_sad + (size_t)(kBm2Waves / NR) * kBm2Cols * (NR * 64 + 4) * 4;
-    l.bytes = l.off_tc + (size_t)kBm2Waves * 64 * 4;               // texture sums per wave
+    l.off_rec = l.off_tc + (size_t)kBm2Waves * 64 * 4;  // texture sums per wave
+    l.bytes = l.off_rec + (size_t)kBm2Waves * 64 * 8;   // per-wave output records
     return l;
 }
 
@@ -324,6 +325,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
     constexpr int SS = NR * 64 + 4;  // slab column stride (dwords)
     uint32_t* sadx = (uint32_t*)(smem + lay.off_sad) + (size_t)cg * kBm2Cols * SS;
     int* tcb = (int*)(smem + lay.off_tc) + wv * 64;
+    uint2* recs = (uint2*)(smem + lay.off_rec) + wv * 64;
     const int f = blockIdx.z;
     const int xl0 = blockIdx.x * BC;
     const int yr0 = e.ymin + blockIdx.y * TY;
@@ -428,10 +430,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
     // scans the disparity indices [16 h, 16 h + 16)
     constexpr int LPC = 4 * NR, CPW = kBm2Cols / NR;
     const int qx = g * CPW + lane / LPC, h = lane % LPC;
-    const int xl = xl0 + c0 + qx;
-    const int ximg = lofs + xl;
-    const bool active = xl < e.ncol;
-    const bool border = !keep_border && (ximg < e.xmin || ximg >= e.xmax);
 
     uint32_t cs[NC];
     uint32_t tc = 0;  // texture column sum of virtual column `lane` (lanes < NC)
@@ -487,6 +485,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // output records: rows t0 .. t0 + cnt - 1 of the wave's CPW columns; lane
+    // (slot, column) = (lane / CPW, lane % CPW)
+    constexpr int RB = LPC;  // rows per flush: RB * CPW = 64
+    auto flush = [&](int t0, int cnt) {
+        wave_sync();  // the h == 0 lanes' records
+        const int slot = lane / CPW, qf = g * CPW + lane % CPW;
+        const int xf = xl0 + c0 + qf, xi = lofs + xf;
+        if (slot < cnt && xf < e.ncol) {
+            const uint2 r = recs[lane];
+            const int y = yr0 + t0 + slot;
+            const int mind = (int)(r.x & 0xffu);
+            const int minsad = (int)((r.x & 0x3fffffffu) >> 8);
+            int16_t res = (int16_t)e.filtered;
+            const bool fail = (!keep_border && (xi < e.xmin || xi >= e.xmax)) || (r.x >> 30) != 0;
+            if (!fail) {
+                const int pp = (int)(r.y & 0xffffu), nn = (int)(r.y >> 16);
+                const int v1 = nd - mind - 1 + e.mindisp;
+                int val;
+                if (0 < mind && mind < nd - 1) {
+                    const int d = pp + nn - 2 * minsad + abs(pp - nn);
+                    val = (v1 * 256 + (d != 0 ? (pp - nn) * 256 / d : 0) + 15) >> 4;
+                } else {
+                    val = (v1 * 256 + 15) >> 4;
+                }
+                res = (int16_t)val;
+                if (cost) cost[((size_t)f * H + y) * W + xi] = minsad;
+            }
+            out[f * ofs + (size_t)y * os + xi] = res;
+        }
     };
     // one row's window SADs, argmin, tests and output
     auto row_out = [&](int t) {
@@ -560,28 +588,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
         int tsum = 0;
 #pragma unroll
         for (int qq = 0; qq < win; qq++) tsum += tcb[qx + qq];
-        const int y = yr0 + t;
-        if (h == 0 && active) {
-            int16_t* op = out + f * ofs + (size_t)y * os + ximg;
-            int16_t res;
-            bool computed = false;
-            if (border || tsum < e.tex || bad) {
-                res = (int16_t)e.filtered;
-            } else {
-                const int v1 = nd - mind - 1 + e.mindisp;
-                int val;
-                if (0 < mind && mind < nd - 1) {
-                    const int d = pp + nn - 2 * (int)minsad + abs(pp - nn);
-                    val = (v1 * 256 + (d != 0 ? (pp - nn) * 256 / d : 0) + 15) >> 4;
-                } else {
-                    val = (v1 * 256 + 15) >> 4;
-                }
-                res = (int16_t)val;
-                computed = true;
-            }
-            *op = res;
-            if (cost && computed) cost[((size_t)f * H + y) * W + ximg] = (int)minsad;
-        }
+        // park the column's verdict; every RB rows the wave's 64 lanes finish
+        // RB x CPW pixels at once (division, stores) instead of 16 / NR lanes
+        // per row
+        if (h == 0)
+            recs[(t & (RB - 1)) * CPW + lane / LPC] =
+                make_uint2(best | (bad ? 1u << 31 : 0u) | (tsum < e.tex ? 1u << 30 : 0u),
+                           ((uint32_t)pp & 0xffffu) | ((uint32_t)nn << 16));
+        if ((t & (RB - 1)) == RB - 1 || t == rows - 1) flush(t & ~(RB - 1), (t & (RB - 1)) + 1);
         group_sync();
     };
     // the whole row walk per addressing variant (no register copies between
@@ -741,7 +755,10 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
             for (int ty = 4; ty <= 64; ty += 4) {
                 const size_t bytes = bm2_layout(e.wsz2, ty, NR).bytes;
                 if (bytes > 160 * 1024) break;
-                const long long k = std::min<long long>(vgpr_blocks, (160 * 1024) / (long long)bytes);
+                // LDS is handed out in 2 KiB steps (measured: 54 208 B per block
+                // gives two resident blocks, not three)
+                const long long k =
+                    std::min<long long>(vgpr_blocks, (160 * 1024) / (long long)((bytes + 2047) & ~(size_t)2047));
                 const long long blocks = (long long)gx * ((nrows + ty - 1) / ty) * n;
                 const long long rounds = (blocks + ctx->cus * k - 1) / (ctx->cus * k);
                 const double c = rounds * (ty + win * 0.25 + 1) * std::pow(4.0 / std::min<long long>(k, 4), 0.6);
