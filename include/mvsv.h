@@ -95,7 +95,11 @@ enum {
     MVSV_OPT_STRIP_SPIN_LIMIT = 1,
     /* rows per block of the StereoBM disparities-on-lanes kernel (0 = chosen
      * per launch from the shape; 1..128 forces it -- tests, A/B runs) */
-    MVSV_OPT_BM_TILE_ROWS = 2
+    MVSV_OPT_BM_TILE_ROWS = 2,
+    /* compute waves per strip of the SGBM sheared-strip kernel: 0 = by launch
+     * size (narrow strips when the wide ones would leave CUs idle), 8 (4 for
+     * numDisparities > 128) = narrow, 15 (7) = wide; other values = 0 */
+    MVSV_OPT_STRIP_WAVES = 3
 };
 
 /* StereoSGBM modes (cv::StereoSGBM::MODE_SGBM / MODE_HH). */

@@ -1197,11 +1197,19 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
 // one extra wave per block does all strip-to-strip traffic, so the compute
 // waves' memory counters only ever wait for their own C loads.
 // ---------------------------------------------------------------------------
-// compute waves per block: 15 (+ the exchange wave = 1024 threads, <= 128 VGPRs)
-// for up to 8 disparities per lane; 7 for D = 256 (16 per lane, ~200 VGPRs)
+// compute waves per block (WV): wide strips, 15 (+ the exchange wave = 1024
+// threads, <= 128 VGPRs) for up to 8 disparities per lane, 7 for D = 256 (16
+// per lane, ~200 VGPRs) -- the throughput shape for frame batches; narrow
+// strips, 8 (4 for D = 256) compute waves -- the latency shape for one or two
+// frames, where wide strips leave most CUs idle and each step of a strip is
+// the serial work of its CU (see launch_tri)
 template <int NP>
+constexpr int tri_wide_waves() { return NP >= 8 ? 7 : 15; }
+template <int NP>
+constexpr int tri_narrow_waves() { return NP >= 8 ? 4 : 8; }
+template <int NP, int WV>
 struct TriCfg {
-    static constexpr int kWaves = NP >= 8 ? 7 : 15;
+    static constexpr int kWaves = WV;
     static constexpr int kSW = 4 * kWaves;  // U-columns per strip
     static constexpr int kThreads = 64 * (kWaves + 1);
 };
@@ -1212,9 +1220,9 @@ constexpr int kTriPF = MVSV_TRI_PF;     // steps of C prefetch (compute waves)
 constexpr int kTriBF = 4;               // steps of boundary prefetch (comm wave)
 constexpr int kTriUnroll = 4;           // lcm(kTriPF, kTriBF, 2)
 
-template <int NP>
+template <int NP, int WV>
 struct TriLayout {
-    static constexpr int kCols = TriCfg<NP>::kSW + 2;  // + two columns of the right strip
+    static constexpr int kCols = TriCfg<NP, WV>::kSW + 2;  // + two columns of the right strip
     // dwords per column, odd: lane (column c, rl) reads / writes element p of
     // its 2*NP disparities at c*kColDw + rl*NP + p, so for NP = 4 the 64 lanes
     // of one b32 access hit 64 distinct banks (c + 4 rl + p mod 64); with the
@@ -1275,8 +1283,8 @@ __device__ __forceinline__ size_t tri_slot(int chain, int k, int t, int nchains,
     return ((((size_t)k * nchains + chain) * H + t) * 4) * 16 * TriGran<NP>::NG;
 }
 
-template <int NP, typename AccT, bool NW = false>
-__global__ __launch_bounds__(TriCfg<NP>::kThreads)
+template <int NP, int WV, typename AccT, bool NW = false>
+__global__ __launch_bounds__((TriCfg<NP, WV>::kThreads))
 __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     const int16_t* __restrict__ C, AccT* __restrict__ A, size_t plane, AccT* __restrict__ dummy,
     int H, int W1, int D, int npass, int P1, int P2, unsigned long long* __restrict__ bnd,
@@ -1284,11 +1292,11 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     int* __restrict__ report, unsigned long long* __restrict__ stats)
 {
     using AV = AccVec<NP, AccT>;
-    using TL = TriLayout<NP>;
+    using TL = TriLayout<NP, WV>;
     using TG = TriGran<NP>;
     constexpr int NG = TG::NG;
-    constexpr int kTriWaves = TriCfg<NP>::kWaves;
-    constexpr int kTriSW = TriCfg<NP>::kSW;
+    constexpr int kTriWaves = TriCfg<NP, WV>::kWaves;
+    constexpr int kTriSW = TriCfg<NP, WV>::kSW;
     constexpr int PF = NP >= 8 ? 2 : kTriPF;  // D = 256: 256 VGPRs already
     constexpr int BF = kTriBF;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2231,12 +2239,12 @@ static bool use_strips(const mvsv_ctx* ctx, const SgbmEff& e, int H)
     return ctx->tri && (size_t)H * e.W1 * e.D < ((size_t)1 << 31);
 }
 
-template <int NP, typename AccT, bool NW>
-int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
-               int npass)
+template <int NP, int WV, typename AccT, bool NW>
+int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
+                  int npass)
 {
-    using TL = TriLayout<NP>;
-    constexpr int kTriSW = TriCfg<NP>::kSW;
+    using TL = TriLayout<NP, WV>;
+    constexpr int kTriSW = TriCfg<NP, WV>::kSW;
     const int nstrips = (e.W1 + H - 1 + kTriSW - 1) / kTriSW;
     const size_t bytes = (size_t)npass * n * nstrips * H * 4 * 16 * TriGran<NP>::NG * 8;
     int rc;
@@ -2269,7 +2277,7 @@ int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT*
         (void)hipMalloc(&stats, (size_t)grid.x * 64);
         (void)hipMemset(stats, 0, (size_t)grid.x * 64);
     }
-    hipLaunchKernelGGL((sgbm_tri_kernel<NP, AccT, NW>), grid, dim3(TriCfg<NP>::kThreads), TL::kBytes,
+    hipLaunchKernelGGL((sgbm_tri_kernel<NP, WV, AccT, NW>), grid, dim3(TriCfg<NP, WV>::kThreads), TL::kBytes,
                        ctx->stream, Cv, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, npass, e.P1,
                        e.P2, (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips,
                        (int*)ctx->status.ptr, ctx->spin_limit, ctx->report_target, stats);
@@ -2301,6 +2309,28 @@ int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT*
         }
     }
     return rc;
+}
+
+// Strip width: wide strips while the launch has at least one block per CU
+// (frame batches: the kernel is VALU-bound and wide strips share the step
+// barrier and the exchange wave among 15 compute waves); narrow strips when it
+// would not (one 640x480 frame: 34 wide blocks on 256 CUs, each strip step the
+// serial VALU work of 15 waves on one CU) -- the chain of strips then spreads
+// over more CUs at about half the per-step work (640x480, one frame: strips
+// 0.62 -> 0.41 ms; 4 waves per strip: 0.42 ms, its longer chain of strips
+// eats the shorter steps).  MVSV_OPT_STRIP_WAVES forces either shape.
+template <int NP, typename AccT, bool NW>
+int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
+               int npass)
+{
+    constexpr int wide = tri_wide_waves<NP>(), narrow = tri_narrow_waves<NP>();
+    int wv = ctx->strip_waves;
+    if (wv != wide && wv != narrow) {
+        const long long blocks = (long long)npass * n * ((e.W1 + H - 1 + 4 * wide - 1) / (4 * wide));
+        wv = blocks < ctx->cus ? narrow : wide;
+    }
+    if (wv == narrow) return launch_tri_wv<NP, narrow, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass);
+    return launch_tri_wv<NP, wide, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass);
 }
 
 // Sheared-strip schedule: the down pass ((1,1) (0,1) (-1,1)), the up pass

@@ -1,0 +1,68 @@
+"""Strip width of the SGBM sheared-strip path kernel (sgbm_tri_kernel, WV
+compute waves per strip): the narrow shape (latency, chosen for one or two
+frames) and the wide shape (throughput, chosen for frame batches) forced on the
+same inputs, both bit-exact against the oracle -- D = 32..128 (8 / 15 waves)
+and D = 256 (4 / 7 waves), 5 and 8 paths, the no-wrap and the general
+recurrence, a frame batch through the device path.
+Reference: Disparity::sgbm (src/disparity.cpp:6-10) -> cv::StereoSGBM::compute."""
+import numpy as np
+import pytest
+
+from tests.test_gpu_parity import rand_pair, report, sgbm_both
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # (H, W, D, blockSize, P1, P2, mode)
+    (61, 200, 64, 5, 8, 32, 1),      # no-wrap, 8 paths
+    (47, 170, 32, 3, 2, 5, 0),       # 5 paths
+    (90, 300, 128, 9, 72, 288, 1),   # sgbm.yml-like P1/P2
+    (40, 160, 64, 11, 300, 4000, 1),  # general (wrapping) recurrence
+    (33, 420, 256, 3, 8, 96, 1),     # D = 256: wide = 7 waves
+]
+
+
+@pytest.mark.parametrize("shape", ["narrow", "wide"])
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_strip_width_forced(gpu, mvsv, oracle, case, shape):
+    from mvstereovision3_amd import _lib
+    H, W, D, bs, P1, P2, mode = CASES[case]
+    waves = {("narrow", False): 8, ("narrow", True): 4, ("wide", False): 15, ("wide", True): 7}[(shape, D > 128)]
+    rng = np.random.default_rng(9100 + 7 * case)
+    L, R = rand_pair(rng, H, W, int(rng.integers(0, min(D, 48))), int(rng.integers(0, 3)))
+    kw = dict(minDisparity=int(rng.integers(-3, 3)), numDisparities=D, blockSize=bs, P1=P1, P2=P2,
+              disp12MaxDiff=1, uniquenessRatio=10, mode=mode)
+    try:
+        _lib.set_option(_lib.OPT_STRIP_WAVES, waves)
+        got, want = sgbm_both(mvsv, oracle, L, R, **kw)
+    finally:
+        _lib.set_option(_lib.OPT_STRIP_WAVES, 0)
+    assert np.array_equal(got, want), f"waves={waves} {kw}: " + report(got, want)
+
+
+def test_strip_width_batch_device(gpu, mvsv, oracle):
+    """Three frames in one launch with narrow strips forced (the automatic
+    choice for small launches is narrow; wide is covered by the 1280x960
+    batch tests)."""
+    from mvstereovision3_amd import _lib
+    torch = gpu
+    rng = np.random.default_rng(9200)
+    H, W, D = 96, 260, 64
+    pairs = [rand_pair(rng, H, W, int(rng.integers(0, 40)), k % 3) for k in range(3)]
+    m = mvsv.StereoSGBM.create(minDisparity=1, numDisparities=D, blockSize=7, P1=8, P2=40,
+                               disp12MaxDiff=1, uniquenessRatio=5, mode=1)
+    dev = torch.device("cuda", 0)
+    Lb = torch.from_numpy(np.stack([q[0] for q in pairs])).to(dev)
+    Rb = torch.from_numpy(np.stack([q[1] for q in pairs])).to(dev)
+    out = torch.empty((3, H, W), dtype=torch.int16, device=dev)
+    try:
+        _lib.set_option(_lib.OPT_STRIP_WAVES, 8)
+        m.compute(Lb, Rb, out)
+        got = out.cpu().numpy()
+    finally:
+        _lib.set_option(_lib.OPT_STRIP_WAVES, 0)
+    p = dict(min_disparity=1, num_disparities=D, block_size=7, p1=8, p2=40, disp12_max_diff=1,
+             pre_filter_cap=0, uniqueness_ratio=5, speckle_window_size=0, speckle_range=0, mode=1)
+    for i, (L, R) in enumerate(pairs):
+        want = oracle.sgbm(L, R, p)
+        assert np.array_equal(got[i], want), f"frame {i}: " + report(got[i], want)
