@@ -269,7 +269,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
         (void)hipGetLastError();
         c->cus = 256;
     }
-    if (const char* v = std::getenv("MVSV_LINES_AUX")) c->lines_aux = std::max(0, std::min(2, std::atoi(v)));
+    if (const char* v = std::getenv("MVSV_LINES_AUX")) c->lines_aux = std::max(-1, std::min(2, std::atoi(v)));
     *out = c;
     return MVSV_OK;
 }

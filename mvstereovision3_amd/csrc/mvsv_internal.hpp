@@ -110,7 +110,7 @@ struct mvsv_ctx {
     int cost_ty = 0;  // cost-volume tile height (0 = by image height); MVSV_COST_TY for A/B runs
     int tri = 1;     // sheared-strip kernels: three directions per sweep
     int strip_waves = 0;  // compute waves per strip (0 = by launch size; 4 or the wide count forces)
-    int lines_aux = 0;  // L->R line kernel on the second stream, beside the strip kernel
+    int lines_aux = -1;  // L->R line kernel beside the strip kernel: -1 = small launches only, 0 / 1 / 2 force
     int bm2 = 1;     // StereoBM: disparities-on-lanes match kernel where blockSize <= 21, D <= 128
     int bm_ty = 0;   // its tile height (0 = chosen per launch); MVSV_BM_TY for A/B runs
     int cus = 256;   // compute units of the device (launch-shape choices)

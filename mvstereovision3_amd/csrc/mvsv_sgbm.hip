@@ -2356,7 +2356,18 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
         if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_fork, s), "fork")) ||
             (rc = check_hip(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0), "fork wait")))
             return rc;
-        hipStream_t ls = ctx->lines_aux ? ctx->aux : s;
+        // lines_aux < 0 (default): beside the strips when the launch is small
+        // (the strips then occupy a fraction of the CUs -- one frame: ~60 of
+        // 256 -- and the L->R lines fill idle ones); after them for batches,
+        // where both kernels saturate the GPU and running them together was
+        // measured slower
+        int aux_mode = ctx->lines_aux;
+        if (aux_mode < 0) {
+            constexpr int wide = tri_wide_waves<NP>();
+            const long long blocks = (long long)npass * n * ((e.W1 + H - 1 + 4 * wide - 1) / (4 * wide));
+            aux_mode = blocks < ctx->cus ? 1 : 0;
+        }
+        hipStream_t ls = aux_mode ? ctx->aux : s;
         auto lines = [&]() {
             StageTimer tl(ctx, kStageLines, ls);
             dim3 grid((num_lines(1, 0, e.W1, H) + 15) / 16, n);
@@ -2366,13 +2377,13 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
         };
         // lines_aux: 0 = after the strip kernel on the same stream, 1 = on the
         // second stream launched before it, 2 = on the second stream after it
-        if (ctx->lines_aux == 1) lines();
+        if (aux_mode == 1) lines();
         if ((rc = check_hip(ctx, hipGetLastError(), "sgbm L->R lines"))) return rc;
         {
             StageTimer ts(ctx, kStageStrips);
             if ((rc = launch_tri<NP, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass))) return rc;
         }
-        if (ctx->lines_aux != 1) lines();
+        if (aux_mode != 1) lines();
         if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_join, ctx->aux), "join")) ||
             (rc = check_hip(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0), "join wait")))
             return rc;
