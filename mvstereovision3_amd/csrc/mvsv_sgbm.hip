@@ -6,7 +6,7 @@
 //   2. sgbm_cost_kernel        Birchfield-Tomasi pixel cost + bs x bs box
 //                              sum -> C[y][x][d] int16 (+P2 bias), LDS-staged
 //                              rows, running vertical sums in registers
-//   3. sgbm_cost_fixup_kernel  OpenCV 3.4's cost-row quirks (column x=0 and
+//   3. sgbm_cost_fixup_*_kernel OpenCV 3.4's cost-row quirks (column x=0 and
 //                              the bottom SH2 rows are not refreshed)
 //   4. sgbm_path_kernel        one wave per scanline of one direction: the
 //                              SGM recurrence on packed int16 pairs
@@ -570,31 +570,43 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
 // 3. OpenCV 3.4 cost-row quirks (see oracle/twin.py sgbm_cost_volume):
 //    rows y >= 1 never refresh column x = 0; rows with y + SH2 >= H are never
 //    recomputed (MODE_SGBM keeps the last computed row, MODE_HH keeps P2).
-__global__ __launch_bounds__(256) void sgbm_cost_fixup_kernel(int16_t* __restrict__ C, int H,
-                                                              SgbmEff e, int ylast, int ybot)
+// Column x = 0 of rows 1 .. ybot - 1 (block per row; not launched with
+// FIRSTCOL_FIX): C(0, 0, d), or P2 in MODE_HH.
+__global__ __launch_bounds__(256) void sgbm_cost_fixup_col0_kernel(int16_t* __restrict__ C, int H,
+                                                                   SgbmEff e)
 {
-    // blockIdx.x enumerates (row y >= 1), threads sweep x*D + d.
     const int y = 1 + blockIdx.x;
     const int f = blockIdx.y;
     const int D = e.D, W1 = e.W1;
-    const bool fix = (e.variant & MVSV_VARIANT_FIRSTCOL_FIX) != 0;
-    const bool bottom = y >= ybot;
-    if (!bottom && fix) return;
     int16_t* Cf = C + (size_t)f * H * W1 * D;
     int16_t* row = Cf + (size_t)y * W1 * D;
-    const int n = bottom ? W1 * D : D;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        int x = i / D;
-        int16_t val;
-        if (e.fullDP) {
-            val = (int16_t)e.P2;
-        } else if (x == 0 && !fix) {
-            val = Cf[i];  // C(0, 0, d)
-        } else {
-            val = Cf[(size_t)ylast * W1 * D + i];
-        }
-        row[i] = val;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) row[d] = e.fullDP ? (int16_t)e.P2 : Cf[d];
+}
+
+// Rows ybot .. H - 1, all columns (grid: 8-element chunks x rows x frames):
+// row ylast (column 0: C(0, 0, d) unless FIRSTCOL_FIX) or P2 (MODE_HH).  D is a
+// multiple of 16, so a 16-byte chunk never straddles two columns.
+__global__ __launch_bounds__(256) void sgbm_cost_fixup_bottom_kernel(int16_t* __restrict__ C, int H,
+                                                                     SgbmEff e, int ylast, int ybot)
+{
+    const int D = e.D, W1 = e.W1;
+    const size_t chunk = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // 8 elements each
+    const size_t rowlen = (size_t)W1 * D;
+    if (chunk * 8 >= rowlen) return;
+    const int y = ybot + blockIdx.y;
+    const int f = blockIdx.z;
+    int16_t* Cf = C + (size_t)f * H * rowlen;
+    uint4* dst = (uint4*)(Cf + (size_t)y * rowlen) + chunk;
+    uint4 v;
+    if (e.fullDP) {
+        const uint32_t p2 = (uint32_t)(e.P2 & 0xffff) * 0x10001u;
+        v = make_uint4(p2, p2, p2, p2);
+    } else {
+        const bool fix = (e.variant & MVSV_VARIANT_FIRSTCOL_FIX) != 0;
+        const bool col0 = chunk * 8 < (size_t)D && !fix;
+        v = *((const uint4*)(Cf + (col0 ? 0 : (size_t)ylast * rowlen)) + chunk);
     }
+    *dst = v;
 }
 
 // ---------------------------------------------------------------------------
@@ -2626,8 +2638,18 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     const int ylast = std::max(H - e.SH2 - 1, 0);  // last recomputed row
     if (H > 1 && !pinned_hh) {
         StageTimer tm(ctx, kStageFixup);
-        hipLaunchKernelGGL(sgbm_cost_fixup_kernel, dim3(H - 1, n), dim3(256), 0, s, Cv, H, e,
-                           ylast, ybot);
+        // OpenCV 3.4 quirks: rows >= 1 never refresh column 0; rows with
+        // y + SH2 >= H are never recomputed (MODE_SGBM keeps the last computed
+        // row, MODE_HH keeps P2).  Column 0 of the bottom rows is written by the
+        // bottom kernel (the rows are disjoint).
+        const bool fix = (e.variant & MVSV_VARIANT_FIRSTCOL_FIX) != 0;
+        if (ybot > 1 && !fix)
+            hipLaunchKernelGGL(sgbm_cost_fixup_col0_kernel, dim3(ybot - 1, n), dim3(256), 0, s, Cv, H, e);
+        if (ybot < H) {
+            const size_t chunks = ((size_t)e.W1 * e.D + 7) / 8;
+            hipLaunchKernelGGL(sgbm_cost_fixup_bottom_kernel, dim3((unsigned)((chunks + 255) / 256), H - ybot, n),
+                               dim3(256), 0, s, Cv, H, e, ylast, ybot);
+        }
         if ((rc = check_hip(ctx, hipGetLastError(), "sgbm cost fixup"))) return rc;
     }
 
