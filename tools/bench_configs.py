@@ -159,6 +159,16 @@ def main():
     mean, med = timed(lambda: m5.compute(L, R, out), K, Wm)
     line("sgbm_1280x960_5path_device_resident", W, H, 128, n, mean, med,
          ("sgbm5", OPS_PER_PXD["sgbm5"] * W * H * 128 * n))
+    # config 5 matcher (liveDisparity: create(0, 256, 9, 648, 2592), MODE_SGBM)
+    # on one frame -- the live-camera latency -- and on the stream's batch of 8,
+    # device-resident (tools/bench_stream.py measures the host-to-host stream)
+    m256 = mvsv.StereoSGBM.create(0, 256, 9, 648, 2592)
+    for n5 in (1, 8):
+        L5, R5 = frames(mvsv, n5, W, H, 0, 256, dev)
+        out5 = torch.empty((n5, H, W), dtype=torch.int16, device=dev)
+        mean, med = timed(lambda: m256.compute(L5, R5, out5), K, Wm)
+        line("config5_sgbm_1280x960_d256_device_resident", W, H, 256, n5, mean, med,
+             ("sgbm5", OPS_PER_PXD["sgbm5"] * W * H * 256 * n5), {"mode": "MODE_SGBM"})
     mvsv.synchronize()
 
 
