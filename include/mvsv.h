@@ -99,7 +99,13 @@ enum {
     /* compute waves per strip of the SGBM sheared-strip kernel: 0 = by launch
      * size (narrow strips when the wide ones would leave CUs idle), 8 (4 for
      * numDisparities > 128) = narrow, 15 (7) = wide; other values = 0 */
-    MVSV_OPT_STRIP_WAVES = 3
+    MVSV_OPT_STRIP_WAVES = 3,
+    /* SGBM path schedule (numDisparities 32 / 64 / 128 / 256): 0 = by launch
+     * size -- all line directions side by side for launches that would fill
+     * at most half the GPU with sheared strips (one camera frame; needs
+     * P2 <= 15),
+     * sheared strips otherwise; 1 = strips; 2 = directions side by side */
+    MVSV_OPT_PATH_SCHEDULE = 4
 };
 
 /* StereoSGBM modes (cv::StereoSGBM::MODE_SGBM / MODE_HH). */

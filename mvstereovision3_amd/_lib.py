@@ -28,6 +28,7 @@ MVSV_E_TIMEOUT = -7
 OPT_STRIP_SPIN_LIMIT = 1
 OPT_BM_TILE_ROWS = 2
 OPT_STRIP_WAVES = 3
+OPT_PATH_SCHEDULE = 4
 
 MODE_SGBM = 0
 MODE_HH = 1

@@ -263,6 +263,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
         if (std::strstr(v, "bm-tile")) c->bm2 = 0;
     }
     if (const char* v = std::getenv("MVSV_COST_TY")) c->cost_ty = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("MVSV_PATH_SCHEDULE")) c->path_sched = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("MVSV_STRIP_WAVES")) c->strip_waves = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("MVSV_BM_TY")) c->bm_ty = std::max(0, std::min(128, std::atoi(v)));
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess) {
@@ -402,6 +403,10 @@ int mvsv_set_option(mvsv_ctx* ctx, int option, long long value)
     case MVSV_OPT_BM_TILE_ROWS:
         if (value < 0 || value > 128) return set_error(ctx, MVSV_E_INVALID_ARG, "BM tile rows must be 0..128");
         ctx->bm_ty = (int)value;
+        return MVSV_OK;
+    case MVSV_OPT_PATH_SCHEDULE:
+        if (value < 0 || value > 2) return set_error(ctx, MVSV_E_INVALID_ARG, "path schedule must be 0..2");
+        ctx->path_sched = (int)value;
         return MVSV_OK;
     case MVSV_OPT_STRIP_WAVES:
         if (value < 0 || value > 64) return set_error(ctx, MVSV_E_INVALID_ARG, "strip waves must be 0..64");

@@ -109,6 +109,7 @@ struct mvsv_ctx {
     int cost2 = 1;   // register-ring cost kernel where blockSize <= 15
     int cost_ty = 0;  // cost-volume tile height (0 = by image height); MVSV_COST_TY for A/B runs
     int tri = 1;     // sheared-strip kernels: three directions per sweep
+    int path_sched = 0;   // 16-lane path schedule: 0 = by launch size, 1 = strips, 2 = directions side by side
     int strip_waves = 0;  // compute waves per strip (0 = by launch size; 4 or the wide count forces)
     int lines_aux = -1;  // L->R line kernel beside the strip kernel: -1 = small launches only, 0 / 1 / 2 force
     int bm2 = 1;     // StereoBM: disparities-on-lanes match kernel where blockSize <= 21, D <= 128

@@ -1116,19 +1116,17 @@ __device__ __forceinline__ uint32_t row_min_u16x2(uint32_t v)
 constexpr int kPath16PF = 12;
 
 template <int NP, bool FIRST, typename AccT, bool NW = false>
-__global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restrict__ C,
-                                                          AccT* __restrict__ A,
-                                                          AccT* __restrict__ dummy, int H, int W1,
-                                                          int D, int dx, int dy, int P1, int P2)
+__device__ __forceinline__ void path16_lines(const int16_t* __restrict__ C, AccT* __restrict__ A,
+                                             AccT* __restrict__ dummy, int H, int W1, int D, int dx,
+                                             int dy, int P1, int P2, int bx, int f)
 {
     using AV = AccVec<NP, AccT>;
     constexpr int PF = kPath16PF;
     const int lane = threadIdx.x & 63;
     const int row = lane >> 4, rl = lane & 15;
     const int nl = num_lines(dx, dy, W1, H);
-    const int line0 = __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + (threadIdx.x >> 6)) * 4);
+    const int line0 = __builtin_amdgcn_readfirstlane((bx * 4 + (int)(threadIdx.x >> 6)) * 4);
     if (line0 >= nl) return;
-    const int f = blockIdx.y;
     const int line = min(line0 + row, nl - 1);
     const Line g = line_geometry(line, dx, dy, W1, H);
     const int len = line0 + row < nl ? g.len : 0;
@@ -1190,6 +1188,34 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
 #pragma unroll
     for (int j = 0; j < PF; j++)
         if (j < rem) body(s + j, j);
+}
+
+
+template <int NP, bool FIRST, typename AccT, bool NW = false>
+__global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restrict__ C,
+                                                          AccT* __restrict__ A,
+                                                          AccT* __restrict__ dummy, int H, int W1,
+                                                          int D, int dx, int dy, int P1, int P2)
+{
+    path16_lines<NP, FIRST, AccT, NW>(C, A, dummy, H, W1, D, dx, dy, P1, P2, blockIdx.x, blockIdx.y);
+}
+
+// All directions of a small launch at once (blockIdx.z = direction k, its
+// deltas into plane k): one frame's 4 or 7 line directions run side by side
+// instead of as sheared strips, whose 480-step chain is the single-frame
+// critical path.
+struct PathDirs {
+    int dx[7], dy[7];
+};
+template <int NP, typename AccT, bool NW>
+__global__ __launch_bounds__(256) void sgbm_pathdirs16_kernel(const int16_t* __restrict__ C,
+                                                              AccT* __restrict__ A, size_t plane,
+                                                              AccT* __restrict__ dummy, int H, int W1,
+                                                              int D, PathDirs dirs, int P1, int P2)
+{
+    const int k = blockIdx.z;
+    path16_lines<NP, true, AccT, NW>(C, acc_add(A, (ptrdiff_t)k * (ptrdiff_t)plane), dummy, H, W1, D,
+                                     dirs.dx[k], dirs.dy[k], P1, P2, blockIdx.x, blockIdx.y);
 }
 
 // ---------------------------------------------------------------------------
@@ -2251,6 +2277,27 @@ static bool use_strips(const mvsv_ctx* ctx, const SgbmEff& e, int H)
     return ctx->tri && (size_t)H * e.W1 * e.D < ((size_t)1 << 31);
 }
 
+// Path schedule of the 16-lane kernels (D = 32 / 64 / 128 / 256):
+// 2 = all line directions side by side (sgbm_pathdirs16_kernel, one 4-bit plane
+// per direction, P2 <= 15) -- the latency shape for launches too small to fill
+// the chip with strips (one camera frame); 1 = sheared strips (batches).
+// ctx->path_sched: 0 = by launch size, 1 / 2 force (tests, A/B).
+static int path_schedule(const mvsv_ctx* ctx, const SgbmEff& e, int H, int n)
+{
+    if (!ctx->path16 || !(e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256)) return 0;
+    const bool dirs_ok = e.P2 <= 15;  // one direction's delta <= P2 fits a nibble
+    if (ctx->path_sched == 2 && dirs_ok) return 2;
+    if (ctx->path_sched == 0 && dirs_ok) {
+        const int wide = e.D > 128 ? 7 : 15;
+        const long long blocks = (long long)(e.fullDP ? 2 : 1) * n * ((e.W1 + H - 1 + 4 * wide - 1) / (4 * wide));
+        // measured: one 640x480 or 1280x960 frame and two 640x480 frames gain
+        // (0.76 -> 0.43, 1.62 -> 1.11, 0.83 -> 0.60 ms); two 1280x960 frames
+        // lose (1.87 -> 1.95 ms: seven planes into the final kernel)
+        if (2 * blocks <= ctx->cus) return 2;
+    }
+    return use_strips(ctx, e, H) ? 1 : 0;
+}
+
 template <int NP, int WV, typename AccT, bool NW>
 int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
                   int npass)
@@ -2479,10 +2526,46 @@ int launch_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* 
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels");
 }
 
+template <int NP, bool NW>
+int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, nib2_t* Av,
+                      int16_t* raw)
+{
+    static const int dirs_sgbm[4][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}};
+    static const int dirs_hh[7][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}, {1, -1}, {0, -1}, {-1, -1}};
+    const int ndir = e.fullDP ? 7 : 4;
+    PathDirs pd{};
+    int maxnl = 0;
+    for (int k = 0; k < ndir; k++) {
+        pd.dx[k] = e.fullDP ? dirs_hh[k][0] : dirs_sgbm[k][0];
+        pd.dy[k] = e.fullDP ? dirs_hh[k][1] : dirs_sgbm[k][1];
+        maxnl = std::max(maxnl, num_lines(pd.dx[k], pd.dy[k], e.W1, H));
+    }
+    const size_t plane = (size_t)n * H * e.W1 * e.D;
+    {
+        StageTimer tm(ctx, kStagePath);
+        hipLaunchKernelGGL((sgbm_pathdirs16_kernel<NP, nib2_t, NW>), dim3((maxnl + 15) / 16, n, ndir), dim3(256),
+                           0, ctx->stream, Cv, Av, plane, (nib2_t*)ctx->dummy.ptr, H, e.W1, e.D, pd, e.P1,
+                           e.P2);
+    }
+    StageTimer tm(ctx, kStageFinal);
+    if (ndir == 7)
+        launch_final16<NP, 7, nib2_t, NW>(ctx, n, H, W, e, Cv, Av, plane, raw);
+    else
+        launch_final16<NP, 4, nib2_t, NW>(ctx, n, H, W, e, Cv, Av, plane, raw);
+    return check_hip(ctx, hipGetLastError(), "sgbm path kernels (directions side by side)");
+}
+
 template <int NP>
 int launch_paths16_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv,
                        void* Av, int16_t* raw)
 {
+    if (path_schedule(ctx, e, H, n) == 2) {
+        int rc;
+        if ((rc = ensure(ctx, ctx->dummy, 512 * 16 * 2 * NP, "sgbm dummy slots"))) return rc;
+        if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
+        if (sgbm_no_wrap(e)) return launch_paths_dirs<NP, true>(ctx, n, H, W, e, Cv, (nib2_t*)Av, raw);
+        return launch_paths_dirs<NP, false>(ctx, n, H, W, e, Cv, (nib2_t*)Av, raw);
+    }
     if (use_strips(ctx, e, H) && acc_is_nib(e)) {
         int rc;
         if ((rc = ensure(ctx, ctx->dummy, 512 * 16 * 2 * NP, "sgbm dummy slots"))) return rc;
@@ -2597,9 +2680,10 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     if ((rc = ensure(ctx, ctx->pre, (size_t)n * 2 * plane * 8, "sgbm BT interval planes"))) return rc;
     if ((rc = ensure(ctx, ctx->cost, (size_t)n * vol * 2, "sgbm cost volume"))) return rc;
     // accumulator planes: one per concurrently written direction group
-    const bool wide16 = ctx->path16 && (e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256);
-    const int nplanes = (wide16 && use_strips(ctx, e, H)) ? (e.fullDP ? 3 : 2) : 1;
-    const bool nib = nplanes > 1 && acc_is_nib(e);  // 4-bit planes on the strip schedule
+    const int sched = path_schedule(ctx, e, H, n);
+    const int nplanes = sched == 2 ? (e.fullDP ? 7 : 4) : sched == 1 ? (e.fullDP ? 3 : 2) : 1;
+    // 4-bit planes: one per direction (side by side) or per strip pass + lines
+    const bool nib = sched == 2 || (nplanes > 1 && acc_is_nib(e));
     if ((rc = ensure(ctx, ctx->agg, nib ? (size_t)nplanes * n * vol / 2
                                         : (size_t)nplanes * n * vol * (acc_is_u8(e) ? 1 : 2),
                      "sgbm path-delta accumulator")))

@@ -36,7 +36,11 @@ def oracle_params(m):
 
 @pytest.fixture
 def restore_spin_limit(mvsv):
+    # the sheared-strip schedule (small launches would run the line directions
+    # side by side, which have no hand-off to give up)
+    mvsv.set_option(mvsv.OPT_PATH_SCHEDULE, 1)
     yield
+    mvsv.set_option(mvsv.OPT_PATH_SCHEDULE, 0)
     mvsv.set_option(mvsv.OPT_STRIP_SPIN_LIMIT, 1 << 20)
     try:
         mvsv.synchronize()

@@ -33,10 +33,12 @@ def test_strip_width_forced(gpu, mvsv, oracle, case, shape):
     kw = dict(minDisparity=int(rng.integers(-3, 3)), numDisparities=D, blockSize=bs, P1=P1, P2=P2,
               disp12MaxDiff=1, uniquenessRatio=10, mode=mode)
     try:
+        _lib.set_option(_lib.OPT_PATH_SCHEDULE, 1)  # strips (small launches would run directions side by side)
         _lib.set_option(_lib.OPT_STRIP_WAVES, waves)
         got, want = sgbm_both(mvsv, oracle, L, R, **kw)
     finally:
         _lib.set_option(_lib.OPT_STRIP_WAVES, 0)
+        _lib.set_option(_lib.OPT_PATH_SCHEDULE, 0)
     assert np.array_equal(got, want), f"waves={waves} {kw}: " + report(got, want)
 
 
@@ -56,11 +58,13 @@ def test_strip_width_batch_device(gpu, mvsv, oracle):
     Rb = torch.from_numpy(np.stack([q[1] for q in pairs])).to(dev)
     out = torch.empty((3, H, W), dtype=torch.int16, device=dev)
     try:
+        _lib.set_option(_lib.OPT_PATH_SCHEDULE, 1)
         _lib.set_option(_lib.OPT_STRIP_WAVES, 8)
         m.compute(Lb, Rb, out)
         got = out.cpu().numpy()
     finally:
         _lib.set_option(_lib.OPT_STRIP_WAVES, 0)
+        _lib.set_option(_lib.OPT_PATH_SCHEDULE, 0)
     p = dict(min_disparity=1, num_disparities=D, block_size=7, p1=8, p2=40, disp12_max_diff=1,
              pre_filter_cap=0, uniqueness_ratio=5, speckle_window_size=0, speckle_range=0, mode=1)
     for i, (L, R) in enumerate(pairs):
