@@ -2710,9 +2710,23 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     } else if (H >= 256) {
         const int TX = cost2_layout(e.D, e.SW2, 120).TX;
         const long tiles_x = (e.W1 + TX - 1) / TX;
-        for (int ty : {120, 96, 64, 48}) {
-            TY = ty;
-            if (tiles_x * ((H + ty - 1) / ty) * n >= 512) break;
+        auto tiles = [&](int ty) { return tiles_x * ((H + ty - 1) / ty) * n; };
+        TY = 120;
+        if (tiles(120) < 1024) {
+            // small launches: least per-CU work, tiles per CU x rows per tile
+            // incl. the 2*SH2 halo, a lone tile on a CU counted 1.5x (8 waves
+            // hide less latency than 16); measured against forced heights: one
+            // 640x480 frame 0.097 -> 0.073 ms, two 0.124 -> 0.110 ms, one
+            // 1280x960 frame 0.227 -> 0.187 ms
+            long best = -1;
+            for (int ty : {120, 96, 64, 48, 32, 24, 16}) {
+                const long per_cu = (tiles(ty) + ctx->cus - 1) / ctx->cus;
+                const long c = per_cu * (ty + 2 * e.SH2) * (per_cu == 1 ? 3 : 2);
+                if (best < 0 || c < best) {
+                    best = c;
+                    TY = ty;
+                }
+            }
         }
     }
     bool pinned_hh = false;
