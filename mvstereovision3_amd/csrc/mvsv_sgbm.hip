@@ -2285,8 +2285,8 @@ static bool use_strips(const mvsv_ctx* ctx, const SgbmEff& e, int H)
 static int path_schedule(const mvsv_ctx* ctx, const SgbmEff& e, int H, int n)
 {
     if (!ctx->path16 || !(e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256)) return 0;
-    const bool dirs_ok = e.P2 <= 15;  // one direction's delta <= P2 fits a nibble
-    if (ctx->path_sched == 2 && dirs_ok) return 2;
+    const bool dirs_ok = e.P2 <= 15 || ctx->path_sched == 2;  // nibble planes; wider planes when forced
+    if (ctx->path_sched == 2) return 2;
     if (ctx->path_sched == 0 && dirs_ok) {
         const int wide = e.D > 128 ? 7 : 15;
         const long long blocks = (long long)(e.fullDP ? 2 : 1) * n * ((e.W1 + H - 1 + 4 * wide - 1) / (4 * wide));
@@ -2526,8 +2526,8 @@ int launch_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* 
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels");
 }
 
-template <int NP, bool NW>
-int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, nib2_t* Av,
+template <int NP, typename AccT, bool NW>
+int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, AccT* Av,
                       int16_t* raw)
 {
     static const int dirs_sgbm[4][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}};
@@ -2543,15 +2543,15 @@ int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int1
     const size_t plane = (size_t)n * H * e.W1 * e.D;
     {
         StageTimer tm(ctx, kStagePath);
-        hipLaunchKernelGGL((sgbm_pathdirs16_kernel<NP, nib2_t, NW>), dim3((maxnl + 15) / 16, n, ndir), dim3(256),
-                           0, ctx->stream, Cv, Av, plane, (nib2_t*)ctx->dummy.ptr, H, e.W1, e.D, pd, e.P1,
+        hipLaunchKernelGGL((sgbm_pathdirs16_kernel<NP, AccT, NW>), dim3((maxnl + 15) / 16, n, ndir), dim3(256),
+                           0, ctx->stream, Cv, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, pd, e.P1,
                            e.P2);
     }
     StageTimer tm(ctx, kStageFinal);
     if (ndir == 7)
-        launch_final16<NP, 7, nib2_t, NW>(ctx, n, H, W, e, Cv, Av, plane, raw);
+        launch_final16<NP, 7, AccT, NW>(ctx, n, H, W, e, Cv, Av, plane, raw);
     else
-        launch_final16<NP, 4, nib2_t, NW>(ctx, n, H, W, e, Cv, Av, plane, raw);
+        launch_final16<NP, 4, AccT, NW>(ctx, n, H, W, e, Cv, Av, plane, raw);
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels (directions side by side)");
 }
 
@@ -2563,8 +2563,15 @@ int launch_paths16_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int
         int rc;
         if ((rc = ensure(ctx, ctx->dummy, 512 * 16 * 2 * NP, "sgbm dummy slots"))) return rc;
         if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
-        if (sgbm_no_wrap(e)) return launch_paths_dirs<NP, true>(ctx, n, H, W, e, Cv, (nib2_t*)Av, raw);
-        return launch_paths_dirs<NP, false>(ctx, n, H, W, e, Cv, (nib2_t*)Av, raw);
+        // one plane per direction: a delta <= P2 in a nibble (4 or 7 of them <= 105
+    // per byte lane), a byte (when all directions' sum fits) or a u16
+        if (e.P2 <= 15) {
+            if (sgbm_no_wrap(e)) return launch_paths_dirs<NP, nib2_t, true>(ctx, n, H, W, e, Cv, (nib2_t*)Av, raw);
+            return launch_paths_dirs<NP, nib2_t, false>(ctx, n, H, W, e, Cv, (nib2_t*)Av, raw);
+        }
+        // the final kernel sums the planes in the plane's element type
+        if (acc_is_u8(e)) return launch_paths_dirs<NP, uint8_t, false>(ctx, n, H, W, e, Cv, (uint8_t*)Av, raw);
+        return launch_paths_dirs<NP, uint16_t, false>(ctx, n, H, W, e, Cv, (uint16_t*)Av, raw);
     }
     if (use_strips(ctx, e, H) && acc_is_nib(e)) {
         int rc;
@@ -2682,10 +2689,12 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     // accumulator planes: one per concurrently written direction group
     const int sched = path_schedule(ctx, e, H, n);
     const int nplanes = sched == 2 ? (e.fullDP ? 7 : 4) : sched == 1 ? (e.fullDP ? 3 : 2) : 1;
-    // 4-bit planes: one per direction (side by side) or per strip pass + lines
-    const bool nib = sched == 2 || (nplanes > 1 && acc_is_nib(e));
+    // 4-bit planes: one per direction (side by side, P2 <= 15) or per strip
+    // pass + lines; bytes / u16 otherwise (side by side: one delta <= P2 each)
+    const bool nib = (sched == 2 && e.P2 <= 15) || (sched == 1 && nplanes > 1 && acc_is_nib(e));
+    const bool u8 = acc_is_u8(e);
     if ((rc = ensure(ctx, ctx->agg, nib ? (size_t)nplanes * n * vol / 2
-                                        : (size_t)nplanes * n * vol * (acc_is_u8(e) ? 1 : 2),
+                                        : (size_t)nplanes * n * vol * (u8 ? 1 : 2),
                      "sgbm path-delta accumulator")))
         return rc;
     if ((rc = ensure(ctx, ctx->raw, (size_t)n * plane * 2, "sgbm raw disparity"))) return rc;

@@ -1,6 +1,7 @@
 """SGBM path schedules of the 16-lane kernels: all line directions side by side
-(sgbm_pathdirs16_kernel, one 4-bit plane per direction -- chosen for launches
-too small to fill the GPU with sheared strips) against the sheared-strip
+(sgbm_pathdirs16_kernel, one plane per direction: 4-bit when P2 <= 15 --
+chosen for launches too small to fill the GPU with sheared strips -- bytes or
+u16 when forced with larger P2) against the sheared-strip
 schedule, both forced on the same inputs and bit-exact against the oracle:
 D = 32 / 64 / 128 / 256, 5 and 8 paths, the no-wrap and the general
 recurrence, uniqueness, a frame batch through the device path.
@@ -20,6 +21,8 @@ CASES = [
     (45, 260, 128, 7, 4, 15, 0),      # largest P2 of the side-by-side schedule
     (40, 420, 256, 9, 2, 5, 1),       # D = 256
     (36, 140, 64, 21, 2, 5, 1),       # general (wrapping) recurrence
+    (48, 220, 128, 5, 8, 100, 1),     # forced side by side: byte planes
+    (40, 330, 256, 9, 648, 2592, 0),  # forced side by side: u16 planes (config 5 params)
 ]
 
 
