@@ -27,9 +27,10 @@ def global_frame_index(rank: int, j: int, frames_per_rank: int) -> int:
     return rank * frames_per_rank + j
 
 
-def gather_frames(out, rank: int, world: int, dst: int = 0) -> Optional[list]:
-    """Gather every rank's (F, H, W) int16 block on ``dst`` (list indexed by rank)."""
-    if world == 1:
+def gather_frames(out, rank: int, world: int, dst: int = 0, collective: bool = False) -> Optional[list]:
+    """Gather every rank's (F, H, W) int16 block on ``dst`` (list indexed by rank).
+    ``collective``: run the collective even for one rank (tests of the RCCL call)."""
+    if world == 1 and not collective:
         return [out]
     import torch
     import torch.distributed as dist
