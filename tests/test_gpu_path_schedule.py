@@ -74,3 +74,8 @@ def test_path_schedule_option_range(gpu):
     for bad in (-1, 3):
         with pytest.raises(_lib.MvsvError):
             _lib.set_option(_lib.OPT_PATH_SCHEDULE, bad)
+    for bad in (-1, 65):
+        with pytest.raises(_lib.MvsvError):
+            _lib.set_option(_lib.OPT_STRIP_WAVES, bad)
+    with pytest.raises(_lib.MvsvError):
+        _lib.set_option(99, 0)  # unknown option
