@@ -134,12 +134,16 @@ __host__ __device__ inline BmLayout bm_layout(int nd, int w2, int sad_bytes)
     return l;
 }
 
+// gsad != nullptr: the per-disparity window sums live in a global scratch slab
+// of this block ([numDisparities][256]) instead of LDS (large numDisparities x
+// blockSize whose LDS image would not fit)
 template <typename SadT>
 __global__ __launch_bounds__(256) void bm_match_kernel(const uint8_t* __restrict__ Lf,
                                                        const uint8_t* __restrict__ Rf, int W,
                                                        int H, BmEff e, int keep_border,
                                                        int16_t* __restrict__ out, size_t os,
-                                                       size_t ofs, int* __restrict__ cost)
+                                                       size_t ofs, int* __restrict__ cost,
+                                                       SadT* __restrict__ gsad)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nd = e.ndisp, w2 = e.wsz2, win = 2 * w2 + 1;
@@ -147,7 +151,8 @@ __global__ __launch_bounds__(256) void bm_match_kernel(const uint8_t* __restrict
     uint8_t* Lt = smem;
     uint8_t* Rt = smem + lay.off_r;
     uint32_t* V = (uint32_t*)(smem + lay.off_v);
-    SadT* sadbuf = (SadT*)(smem + lay.off_sad);
+    const size_t blk = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    SadT* sadbuf = gsad ? gsad + blk * (size_t)e.ndisp * 256 : (SadT*)(smem + lay.off_sad);
     const int NJ = lay.NJ, NRW = lay.NRW, NRC = lay.NRC;
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     const int f = blockIdx.z;
@@ -789,25 +794,33 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
     }
     const bool small = (long long)win * win * 2 * e.cap <= 65535;
     BmLayout lay = bm_layout(e.ndisp, e.wsz2, small ? 2 : 4);
-    if (lay.bytes > 160 * 1024)
-        return set_error(ctx, MVSV_E_INVALID_ARG,
-                         "numDisparities x blockSize too large for the GPU BM kernel");
     dim3 grid((e.ncol + 15) / 16, (e.ymax - e.ymin + 15) / 16, n);
-    if (lay.bytes > 65536) {
+    void* gsad = nullptr;
+    size_t lds = lay.bytes;
+    if (lay.bytes > 160 * 1024) {
+        // window sums in a global scratch slab per block (the LDS keeps the tiles)
+        lds = lay.off_sad;
+        const size_t bytes = (size_t)grid.x * grid.y * grid.z * e.ndisp * 256 * (small ? 2 : 4);
+        if ((rc = ensure(ctx, ctx->bm_sad, bytes, "bm window-sum scratch"))) return rc;
+        gsad = ctx->bm_sad.ptr;
+    }
+    if (lds > 160 * 1024)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "blockSize too large for the GPU BM kernel");
+    if (lds > 65536) {
         const void* fn = small ? (const void*)bm_match_kernel<uint16_t>
                                : (const void*)bm_match_kernel<uint32_t>;
         if ((rc = check_hip(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)lay.bytes),
+                                                     (int)lds),
                             "bm LDS attribute")))
             return rc;
     }
     StageTimer tm(ctx, kStageBm);
     if (small)
-        hipLaunchKernelGGL(bm_match_kernel<uint16_t>, grid, dim3(256), lay.bytes, s, Lf, Rf, W, H,
-                           e, validate ? 1 : 0, out, os, ofs, cost);
+        hipLaunchKernelGGL(bm_match_kernel<uint16_t>, grid, dim3(256), lds, s, Lf, Rf, W, H,
+                           e, validate ? 1 : 0, out, os, ofs, cost, (uint16_t*)gsad);
     else
-        hipLaunchKernelGGL(bm_match_kernel<uint32_t>, grid, dim3(256), lay.bytes, s, Lf, Rf, W, H,
-                           e, validate ? 1 : 0, out, os, ofs, cost);
+        hipLaunchKernelGGL(bm_match_kernel<uint32_t>, grid, dim3(256), lds, s, Lf, Rf, W, H,
+                           e, validate ? 1 : 0, out, os, ofs, cost, (uint32_t*)gsad);
     if ((rc = check_hip(ctx, hipGetLastError(), "bm match"))) return rc;
     return bm_finish(ctx, n, W, H, e, out, os, ofs, cost);
 }

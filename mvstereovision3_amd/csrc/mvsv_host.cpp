@@ -290,7 +290,7 @@ int mvsv_trim(mvsv_ctx* ctx)
     DevBuf* all[] = {&ctx->pre, &ctx->cost, &ctx->agg, &ctx->raw, &ctx->uf_parent, &ctx->uf_size,
                      &ctx->uf_tile, &ctx->tri_bnd, &ctx->status,
                      &ctx->dummy, &ctx->keys,
-                     &ctx->bm_lf, &ctx->bm_rf, &ctx->bm_cost, &ctx->h_left, &ctx->h_right,
+                     &ctx->bm_lf, &ctx->bm_rf, &ctx->bm_cost, &ctx->bm_sad, &ctx->h_left, &ctx->h_right,
                      &ctx->h_out};
     for (DevBuf* b : all) free_buf(*b);
     return MVSV_OK;

@@ -116,7 +116,7 @@ struct mvsv_ctx {
     int bm_ty = 0;   // its tile height (0 = chosen per launch); MVSV_BM_TY for A/B runs
     int cus = 256;   // compute units of the device (launch-shape choices)
     // BM
-    mvsv::DevBuf bm_lf, bm_rf, bm_cost;
+    mvsv::DevBuf bm_lf, bm_rf, bm_cost, bm_sad;
     // host-pointer staging
     mvsv::DevBuf h_left, h_right, h_out;
     // stage profiling (HIP events on the context stream)

@@ -92,10 +92,11 @@ def test_bm_lanes_batch_device(gpu, mvsv, oracle):
         assert np.array_equal(got[i], want), f"frame {i}: " + report(got[i], want)
 
 
-@pytest.mark.parametrize("bs,D", [(23, 32), (25, 144), (9, 160)])
+@pytest.mark.parametrize("bs,D", [(23, 32), (25, 144), (9, 160), (25, 160), (31, 256)])
 def test_bm_general_kernel(gpu, mvsv, oracle, bs, D):
     """Shapes outside the lanes kernel (blockSize > 21 or D > 128) keep the
-    16x16-tile kernel."""
+    16x16-tile kernel; (25, 160) and (31, 256) keep their window sums in a
+    global scratch slab (the LDS image would exceed 160 KB)."""
     rng = np.random.default_rng(8000 + bs + D)
     H, W = 80, D + 150
     p = rand_params(rng, bs, D)
