@@ -43,6 +43,6 @@ def run(name, m, W, H, D, n, steps=30):
 
 cfg3 = mvsv.StereoSGBM.create(1, 128, 13, 0, 0, 0, 0, 0, 150, 2, 1)
 cfg5 = mvsv.StereoSGBM.create(0, 256, 9, 648, 2592)
-for n in (1, 2):
+for n in (1, 2, 8):
     run("config3_640x480_8path", cfg3, 640, 480, 128, n)
     run("config5_1280x960_d256", cfg5, 1280, 960, 256, n)
