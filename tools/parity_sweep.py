@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--sgbm", type=int, default=200)
     ap.add_argument("--bm", type=int, default=200)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--large", type=int, default=0,
+                    help="extra SGBM cases at 640x480 / 1280x960 with 4-8 frame batches")
     a = ap.parse_args()
     import torch
 
@@ -95,6 +97,27 @@ def main():
             jobs.append((tag, got[j], pool.submit(pyoracle.sgbm, L, R, p, variant)))
     _lib.set_option(_lib.OPT_PATH_SCHEDULE, 0)
     _lib.set_option(_lib.OPT_STRIP_WAVES, 0)
+
+    for i in range(a.large):  # batch shapes: wide strips, lines after the strips
+        W, H = (640, 480) if rng.integers(0, 3) else (1280, 960)
+        n = int(rng.choice([4, 8])) if W == 640 else int(rng.choice([2, 4]))
+        D = int(rng.choice([64, 128, 256]))
+        kw = dict(minDisparity=int(rng.integers(-4, 4)), numDisparities=D,
+                  blockSize=int(rng.choice([3, 5, 9, 13])), P1=int(rng.choice([0, 8, 648])),
+                  P2=int(rng.choice([0, 32, 2592])), disp12MaxDiff=int(rng.integers(-1, 3)),
+                  preFilterCap=int(rng.choice([0, 31, 63])), uniquenessRatio=int(rng.choice([0, 10])),
+                  speckleWindowSize=int(rng.choice([0, 150])), speckleRange=2, mode=int(rng.integers(0, 2)))
+        m = mvsv.StereoSGBM.create(**kw)
+        pairs = [mvsv.synth_pair(int(rng.integers(0, 1 << 30)), W, H, max(kw["minDisparity"], 0), D)
+                 for _ in range(n)]
+        Lb = torch.from_numpy(np.stack([q[0] for q in pairs])).to(dev)
+        Rb = torch.from_numpy(np.stack([q[1] for q in pairs])).to(dev)
+        out = torch.empty((n, H, W), dtype=torch.int16, device=dev)
+        m.compute(Lb, Rb, out)
+        got = out.cpu().numpy()
+        p = {k: v for k, v in m.params().items() if k != "variant"}
+        for j, (L, R) in enumerate(pairs):
+            jobs.append((f"large #{i} frame {j}/{n} {W}x{H} {kw}", got[j], pool.submit(pyoracle.sgbm, L, R, p)))
 
     for i in range(a.bm):
         H, W = int(rng.integers(24, 200)), int(rng.integers(80, 400))
