@@ -43,19 +43,16 @@ if ROOT not in sys.path:
 SEED0 = 0x5EED0000
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SGBM_YML = os.path.join(ROOT, "tests", "golden", "configs", "sgbm.yml")
-PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
+PMC_FILE = os.path.join(PROFILE_DIR, "pmc_traffic.json")  # tools/pmc_traffic.py
+SQ_FILE = os.path.join(PROFILE_DIR, "sq_summary.json")    # tools/sq_summary.py
 KERNEL_SOURCES = os.path.join(ROOT, "mvstereovision3_amd", "csrc")
 CPU_SHARE = 16  # host cores of one GPU's share on the GPU box
 
-# what bounds each stage (measured); HBM is the roofline quoted
-# because MFMA is unused (integer min/add work, no dense contraction)
-LIMITER = {
-    "path_strips": "VALU issue + strip-chain critical path (three recurrences per byte of C)",
-    "cost_volume": "latency (VALU ~37 %, LDS ~40 % busy)",
-    "final_wta_lr": "VALU issue",
-    "path_lines": "HBM",
-    "post_filters": "launch / atomics",
-}
+# MFMA is unused (integer min/add work, no dense contraction): a kernel is
+# bound by HBM or by VALU issue; roofline.bound names the larger of the two
+# MEASURED utilisations (PMC traffic / peak, SQ VALU busy cycles / SIMD cycles)
+# of the dominant kernel, from summaries of the same kernel sources.
 
 
 def parse(argv=None):
@@ -71,6 +68,9 @@ def parse(argv=None):
                     help="CPU baseline threads (0 = the GPU's host-core share, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--force-gather", action="store_true",
+                    help="run the multi-rank path even for --gpus 1: torch.distributed.run "
+                         "child, NCCL (RCCL) process group, dist.gather of the maps every step")
     ap.add_argument("--dry", action="store_true",
                     help="CPU rehearsal of launcher + gather (gloo, trivial compute)")
     return ap.parse_args(argv)
@@ -134,6 +134,22 @@ def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True):
         "final_wta_lr": final_b,
         "post_filters": F * 4 * px,
     }.get(stage, 0)
+
+
+def _summary(path, workload, sha, what):
+    """A committed counter summary, only if it is of this workload and these
+    kernel sources: (dict or None, provenance note)."""
+    if not os.path.exists(path):
+        return None, f"no {what} summary ({os.path.relpath(path, ROOT)} absent)"
+    try:
+        js = json.load(open(path))
+    except (OSError, ValueError):
+        return None, f"{what} summary unreadable"
+    if js.get("workload") != workload:
+        return None, f"{what} summary is for another workload"
+    if js.get("kernel_source_sha") != sha:
+        return None, f"{what} summary is stale (kernel sources changed since)"
+    return js, f"{os.path.relpath(path, ROOT)}, kernel sources {sha}"
 
 
 def kernel_source_sha() -> str:
@@ -233,7 +249,7 @@ def dry_main(args, world, rank):
 
 def main(argv=None):
     args = parse(argv)
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.force_gather):
         return launch_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -253,7 +269,8 @@ def main(argv=None):
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    distributed = world > 1 or args.force_gather
+    if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
     W, H, F = args.width, args.height, args.frames
@@ -276,12 +293,13 @@ def main(argv=None):
     Lt = torch.from_numpy(np.stack([h[0] for h in host])).to(dev)
     Rt = torch.from_numpy(np.stack([h[1] for h in host])).to(dev)
     out = torch.empty((F, H, W), dtype=torch.int16, device=dev)
-    gather = world > 1 and not args.no_gather
-    batch = FrameBatch(Lt, Rt, out, lambda L, R, o: m.compute(L, R, o), rank, world, gather)
+    gather = distributed and not args.no_gather
+    batch = FrameBatch(Lt, Rt, out, lambda L, R, o: m.compute(L, R, o), rank, world, gather,
+                       collective=args.force_gather)
 
     def barrier():
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if distributed:
             dist.barrier(device_ids=[local])
         torch.cuda.synchronize(dev)
 
@@ -306,10 +324,15 @@ def main(argv=None):
     _lib.synchronize(local)  # no map of the timed steps came from a given-up hand-off
     elapsed = t1 - t0
     step_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(K)]
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # the gathered global batch of the last timed step, on rank 0 (host copy,
+    # outside the timed region) for the parity sample below
+    gathered = None
+    if gather and rank == 0 and batch.gathered is not None:
+        gathered = [g.cpu().numpy() for g in batch.gathered]
 
     if rank == 0:
         ms_per_step = elapsed / K * 1e3
@@ -329,19 +352,23 @@ def main(argv=None):
         alg_bytes_per_launch = comp * F / launches
         achieved = alg_bytes_per_launch / avg_launch_s / 1e9
         impl_bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir, acc, strips) / launches
-        traffic, traffic_note = None, "no PMC summary for this workload"
-        if os.path.exists(PMC_FILE):
-            try:
-                pmc = json.load(open(PMC_FILE))
-                if pmc.get("workload") != f"sgbm_{W}x{H}_d{D}_{ndir}path_batch{F}":
-                    traffic_note = "PMC summary is for another workload"
-                elif pmc.get("kernel_source_sha") != kernel_source_sha():
-                    traffic_note = "PMC summary is stale (kernel sources changed since)"
-                else:
-                    traffic = pmc.get("stages", {}).get(dom, {}).get("hbm_bytes_per_launch")
-                    traffic_note = f"{os.path.relpath(PMC_FILE, ROOT)} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same kernel sources)"
-            except (OSError, ValueError):
-                traffic = None
+        workload = f"sgbm_{W}x{H}_d{D}_{ndir}path_batch{F}"
+        sha = kernel_source_sha()
+        pmc, traffic_note = _summary(PMC_FILE, workload, sha, "PMC")
+        traffic = pmc.get("stages", {}).get(dom, {}).get("hbm_bytes_per_launch") if pmc else None
+        if pmc:
+            traffic_note += " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE in separate passes)"
+        sq, sq_note = _summary(SQ_FILE, workload, sha, "SQ")
+        valu_frac = sq.get("stages", {}).get(dom, {}).get("valu_util") if sq else None
+        if sq:
+            sq_note += " (rocprofv3 SQ_ACTIVE_INST_VALU x4 / (1024 SIMDs x GRBM_GUI_ACTIVE/8))"
+        # measured HBM utilisation of the dominant kernel: counter bytes over its
+        # live launch time, against the same peak
+        hbm_util = traffic / avg_launch_s / 1e9 / HBM_PEAK_GBPS if traffic else None
+        if valu_frac is not None and hbm_util is not None:
+            bound = "valu" if valu_frac > hbm_util else "hbm"
+        else:
+            bound = "unmeasured"
         res = {
             "metric": "Mpix disparities/sec (SGBM 128-disp, 8-path) at 1/2/4/8 GPUs; % HBM roofline",
             "value": round(mpix, 2),
@@ -361,11 +388,19 @@ def main(argv=None):
                        "block_size": params["block_size"], "mode": "MODE_HH" if args.mode == 1 else "MODE_SGBM",
                        "paths": ndir, "frames_per_gpu": F, "global_batch": F * world,
                        "params": "configs/sgbm.yml + mode", "gather": "rccl" if gather else "none",
+                       "launch": "torch.distributed.run" if distributed else "single process",
                        "parallelism": f"frame-parallel x{world}"},
-            "roofline": {"kernel": dom, "bound": "hbm", "limiter": LIMITER.get(dom, ""),
+            "roofline": {"kernel": dom, "bound": bound,
+                         "bound_rule": "larger of the measured utilisations hbm_util (PMC traffic) and "
+                                       "valu_frac (SQ counters) of the dominant kernel",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "traffic_source": traffic_note,
+                         "hbm_util": round(hbm_util, 4) if hbm_util is not None else None,
+                         "valu_frac": valu_frac,
+                         "valu_source": sq_note,
+                         "pipeline_frac": round(comp * F * K / elapsed / 1e9 / HBM_PEAK_GBPS, 5),
+                         "pipeline_frac_rule": "SURVEY.md §8(d) bytes of the whole step over its wall time / peak",
                          "algorithmic_bytes_per_launch": int(alg_bytes_per_launch),
                          "algorithmic_bytes": "SURVEY.md §8(d): 4*W*H*(1+D) per frame x frames per launch",
                          "avg_launch_ms": round(avg_launch_s * 1e3, 4),
@@ -397,8 +432,18 @@ def main(argv=None):
                                    "latency_1core_s": round(lat, 3),
                                    "host": info}
             res["parity_sample"] = f"{same}/{nchk} frames bit-exact vs oracle"
+        if gathered is not None:
+            # the gathered global batch: frame 0 of every rank, as it arrived on
+            # rank 0, against the oracle (outside the timed region)
+            sample = [(r, mvsv.synth_pair(frame_seeds(r, world, F, SEED0)[0], W, H, minD, D))
+                      for r in range(world)]
+            thr = max(1, min(CPU_SHARE, cpu_info()["affinity"], world))
+            _, ref = cpu_baseline([p for _, p in sample], params, thr)
+            ok = sum(int(np.array_equal(gathered[r][0], ref[i])) for i, (r, _) in enumerate(sample))
+            res["parity_sample_gathered"] = (f"{ok}/{world} gathered frames (frame 0 of each rank, "
+                                             f"received on rank 0 through dist.gather) bit-exact vs oracle")
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
     return 0
 

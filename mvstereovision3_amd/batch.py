@@ -45,15 +45,18 @@ class FrameBatch:
     """Holds one rank's frames and runs compute + gather per step."""
 
     def __init__(self, left, right, out, compute: Callable, rank: int = 0, world: int = 1,
-                 gather: bool = True, dst: int = 0):
+                 gather: bool = True, dst: int = 0, collective: bool = False):
+        """``collective``: gather through the process group even for one rank
+        (bench.py --force-gather runs the multi-rank code path on one GPU)."""
         self.left, self.right, self.out = left, right, out
         self.compute = compute
         self.rank, self.world, self.dst = rank, world, dst
-        self.gather = gather and world > 1
+        self.collective = collective
+        self.gather = gather and (world > 1 or collective)
         self.gathered: Optional[Sequence] = None
 
     def step(self):
         self.compute(self.left, self.right, self.out)
         if self.gather:
-            self.gathered = gather_frames(self.out, self.rank, self.world, self.dst)
+            self.gathered = gather_frames(self.out, self.rank, self.world, self.dst, self.collective)
         return self.gathered

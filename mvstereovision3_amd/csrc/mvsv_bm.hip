@@ -134,16 +134,21 @@ __host__ __device__ inline BmLayout bm_layout(int nd, int w2, int sad_bytes)
     return l;
 }
 
+// bound on the general kernel's global window-sum scratch (per launch)
+constexpr size_t kBmScratchBytes = (size_t)64 << 20;
+
 // gsad != nullptr: the per-disparity window sums live in a global scratch slab
 // of this block ([numDisparities][256]) instead of LDS (large numDisparities x
-// blockSize whose LDS image would not fit)
+// blockSize whose LDS image would not fit).  The slab is indexed by the block
+// of this launch; the host splits such grids into launches of a bounded block
+// count (row-tile offset by0, frame f0), so the scratch stays bounded.
 template <typename SadT>
 __global__ __launch_bounds__(256) void bm_match_kernel(const uint8_t* __restrict__ Lf,
                                                        const uint8_t* __restrict__ Rf, int W,
                                                        int H, BmEff e, int keep_border,
                                                        int16_t* __restrict__ out, size_t os,
                                                        size_t ofs, int* __restrict__ cost,
-                                                       SadT* __restrict__ gsad)
+                                                       SadT* __restrict__ gsad, int by0, int f0)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nd = e.ndisp, w2 = e.wsz2, win = 2 * w2 + 1;
@@ -155,9 +160,9 @@ __global__ __launch_bounds__(256) void bm_match_kernel(const uint8_t* __restrict
     SadT* sadbuf = gsad ? gsad + blk * (size_t)e.ndisp * 256 : (SadT*)(smem + lay.off_sad);
     const int NJ = lay.NJ, NRW = lay.NRW, NRC = lay.NRC;
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-    const int f = blockIdx.z;
+    const int f = f0 + (int)blockIdx.z;
     const int xl0 = blockIdx.x * 16;
-    const int yr0 = e.ymin + blockIdx.y * 16;
+    const int yr0 = e.ymin + (by0 + (int)blockIdx.y) * 16;
     const int lofs = e.lofs, rofs = e.rofs;
     const uint8_t* Lfr = Lf + (size_t)f * W * H;
     const uint8_t* Rfr = Rf + (size_t)f * W * H;
@@ -797,11 +802,17 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
     dim3 grid((e.ncol + 15) / 16, (e.ymax - e.ymin + 15) / 16, n);
     void* gsad = nullptr;
     size_t lds = lay.bytes;
+    // row tiles per launch (all of them unless the window sums go to scratch)
+    int rows_per_launch = (int)grid.y;
     if (lay.bytes > 160 * 1024) {
-        // window sums in a global scratch slab per block (the LDS keeps the tiles)
+        // window sums in a global scratch slab per block (the LDS keeps the
+        // tiles); launches of at most kBmScratchBytes of slab, one frame and a
+        // band of row tiles each, reuse the slab in stream order
         lds = lay.off_sad;
-        const size_t bytes = (size_t)grid.x * grid.y * grid.z * e.ndisp * 256 * (small ? 2 : 4);
-        if ((rc = ensure(ctx, ctx->bm_sad, bytes, "bm window-sum scratch"))) return rc;
+        const size_t per_block = (size_t)e.ndisp * 256 * (small ? 2 : 4);
+        const size_t per_row = per_block * grid.x;
+        rows_per_launch = (int)std::max<size_t>(1, std::min<size_t>(grid.y, kBmScratchBytes / per_row));
+        if ((rc = ensure(ctx, ctx->bm_sad, per_row * rows_per_launch, "bm window-sum scratch"))) return rc;
         gsad = ctx->bm_sad.ptr;
     }
     if (lds > 160 * 1024)
@@ -815,12 +826,25 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
             return rc;
     }
     StageTimer tm(ctx, kStageBm);
-    if (small)
-        hipLaunchKernelGGL(bm_match_kernel<uint16_t>, grid, dim3(256), lds, s, Lf, Rf, W, H,
-                           e, validate ? 1 : 0, out, os, ofs, cost, (uint16_t*)gsad);
-    else
-        hipLaunchKernelGGL(bm_match_kernel<uint32_t>, grid, dim3(256), lds, s, Lf, Rf, W, H,
-                           e, validate ? 1 : 0, out, os, ofs, cost, (uint32_t*)gsad);
+    if (!gsad) {
+        if (small)
+            hipLaunchKernelGGL(bm_match_kernel<uint16_t>, grid, dim3(256), lds, s, Lf, Rf, W, H,
+                               e, validate ? 1 : 0, out, os, ofs, cost, (uint16_t*)nullptr, 0, 0);
+        else
+            hipLaunchKernelGGL(bm_match_kernel<uint32_t>, grid, dim3(256), lds, s, Lf, Rf, W, H,
+                               e, validate ? 1 : 0, out, os, ofs, cost, (uint32_t*)nullptr, 0, 0);
+    } else {
+        for (int f = 0; f < n; f++)
+            for (int by = 0; by < (int)grid.y; by += rows_per_launch) {
+                const dim3 g(grid.x, std::min(rows_per_launch, (int)grid.y - by), 1);
+                if (small)
+                    hipLaunchKernelGGL(bm_match_kernel<uint16_t>, g, dim3(256), lds, s, Lf, Rf, W, H, e,
+                                       validate ? 1 : 0, out, os, ofs, cost, (uint16_t*)gsad, by, f);
+                else
+                    hipLaunchKernelGGL(bm_match_kernel<uint32_t>, g, dim3(256), lds, s, Lf, Rf, W, H, e,
+                                       validate ? 1 : 0, out, os, ofs, cost, (uint32_t*)gsad, by, f);
+            }
+    }
     if ((rc = check_hip(ctx, hipGetLastError(), "bm match"))) return rc;
     return bm_finish(ctx, n, W, H, e, out, os, ofs, cost);
 }

@@ -18,6 +18,9 @@ namespace mvsv {
 
 constexpr int kCost2Threads = 512;
 constexpr int kCost2Run = 4;
+// tile heights sgbm_device picks from (images >= 256 rows; 16 below that);
+// tests/cpp/cost_layout_check.cpp bounds-checks every one of them
+constexpr int kCostTileHeights[] = {120, 96, 64, 48, 32, 24, 16};
 
 struct Cost2Layout {
     int PP, CL, TX, TY, NX, PS, nQmax, qhalf;

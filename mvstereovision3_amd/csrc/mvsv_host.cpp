@@ -55,12 +55,23 @@ int ensure(mvsv_ctx* ctx, DevBuf& b, size_t bytes, const char* what)
 int check_report(mvsv_ctx* ctx)
 {
     if (!ctx->report) return MVSV_OK;
-    const int v = __atomic_load_n(ctx->report, __ATOMIC_ACQUIRE);
+    // one read-and-clear: a give-up stored by a launch still in flight between a
+    // separate load and store would be erased unreported
+    const int v = __atomic_exchange_n(ctx->report, 0, __ATOMIC_ACQ_REL);
     if (v == 0) return MVSV_OK;
-    __atomic_store_n(ctx->report, 0, __ATOMIC_RELEASE);
     return set_error(ctx, MVSV_E_TIMEOUT,
                      "sgbm path kernel: a strip-boundary wait gave up (that launch's maps are all "
                      "INVALID)");
+}
+
+int mark_last_use(mvsv_ctx* ctx, int rc)
+{
+    if (hipEventRecord(ctx->ev_last, ctx->stream) != hipSuccess) {
+        (void)hipGetLastError();
+        return rc ? rc : set_error(ctx, MVSV_E_HIP, "last-use event record failed");
+    }
+    ctx->last_valid = true;
+    return rc;
 }
 
 int alloc_report(mvsv_ctx* ctx, int count, int** host, int** dev)
@@ -242,10 +253,10 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
     c->device = hip_device;
     DeviceGuard dev_guard(hip_device);
     if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_switch, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming) != hipSuccess ||
         alloc_report(c, 1, &c->report, &c->report_dev) != MVSV_OK) {
         (void)hipGetLastError();
-        if (c->ev_switch) (void)hipEventDestroy(c->ev_switch);
+        if (c->ev_last) (void)hipEventDestroy(c->ev_last);
         if (c->own) (void)hipStreamDestroy(c->own);
         delete c;
         return MVSV_E_HIP;
@@ -355,7 +366,7 @@ void mvsv_destroy(mvsv_ctx* ctx)
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-    if (ctx->ev_switch) (void)hipEventDestroy(ctx->ev_switch);
+    if (ctx->ev_last) (void)hipEventDestroy(ctx->ev_last);
     if (ctx->report) (void)hipHostFree(ctx->report);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
@@ -365,16 +376,18 @@ void mvsv_destroy(mvsv_ctx* ctx)
 const char* mvsv_last_error(const mvsv_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 // Every launch of a context shares its cached buffers, so work enqueued on a
-// new stream must not start before the work already on the previous one: the
-// new stream waits on an event recorded on the old (no host synchronisation).
+// new stream must not start before the context's work already enqueued: the
+// new stream waits on the context's last-use event (recorded by the entry
+// points themselves, so neither the previous stream handle -- possibly
+// destroyed by its owner since -- nor unrelated work queued on it is touched).
 static int switch_stream(mvsv_ctx* ctx, hipStream_t s)
 {
     if (s == ctx->stream) return MVSV_OK;
     DeviceGuard dev_guard(ctx->device);
-    int rc;
-    if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_switch, ctx->stream), "stream switch record")) ||
-        (rc = check_hip(ctx, hipStreamWaitEvent(s, ctx->ev_switch, 0), "stream switch wait")))
-        return rc;
+    if (ctx->last_valid) {
+        int rc = check_hip(ctx, hipStreamWaitEvent(s, ctx->ev_last, 0), "stream switch wait");
+        if (rc) return rc;
+    }
     ctx->stream = s;
     return MVSV_OK;
 }
@@ -455,7 +468,7 @@ int mvsv_sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t l
     // maps are INVALID; say so before anything else runs on this context
     if ((rc = check_report(ctx))) return rc;
     DeviceGuard dev_guard(ctx->device);
-    return sgbm_device(ctx, n, L, ls, lfs, R, rs, rfs, W, H, e, out, os, ofs);
+    return mark_last_use(ctx, sgbm_device(ctx, n, L, ls, lfs, R, rs, rfs, W, H, e, out, os, ofs));
 }
 
 int mvsv_bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs,
@@ -471,7 +484,7 @@ int mvsv_bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs
     int rc = resolve_bm(p, W, H, &e, &why);
     if (rc) return set_error(ctx, rc, why);
     DeviceGuard dev_guard(ctx->device);
-    return bm_device(ctx, n, L, ls, lfs, R, rs, rfs, W, H, e, out, os, ofs);
+    return mark_last_use(ctx, bm_device(ctx, n, L, ls, lfs, R, rs, rfs, W, H, e, out, os, ofs));
 }
 
 int mvsv_mean_disparity_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st,
@@ -481,7 +494,7 @@ int mvsv_mean_disparity_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap, s
     if (n <= 0 || !dmap || !means || W <= 0 || H <= 0 || st < (size_t)W)
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad mean-grid arguments");
     DeviceGuard dev_guard(ctx->device);
-    return mean_grid_device(ctx, n, dmap, st, fs, W, H, means);
+    return mark_last_use(ctx, mean_grid_device(ctx, n, dmap, st, fs, W, H, means));
 }
 
 // Host-pointer path: stage through cached device buffers, run, copy back, sync.
@@ -517,7 +530,9 @@ static int host_call(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* 
     if (rc) return rc;
     if ((rc = check_hip(ctx, hipMemcpy2DAsync(out, os * 2, dout, (size_t)W * 2, (size_t)W * 2, H, hipMemcpyDeviceToHost, s), "D2H out"))) return rc;
     if ((rc = check_hip(ctx, hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
-    return check_report(ctx);
+    // only an SGBM call reads the sticky give-up word: a BM call's valid map is
+    // returned and the word waits for the next SGBM call or mvsv_synchronize
+    return sgbm ? check_report(ctx) : MVSV_OK;
 }
 
 int mvsv_sgbm(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* R, size_t rs, int W,
@@ -543,7 +558,7 @@ int mvsv_reproject_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, 
     if (n <= 0 || !dmap || !Q || !xyzw || W <= 0 || H <= 0 || st < (size_t)W || xs < (size_t)W)
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad reprojection arguments");
     DeviceGuard dev_guard(ctx->device);
-    return reproject_device(ctx, n, dmap, st, fs, W, H, Q, xyzw, xs, xfs);
+    return mark_last_use(ctx, reproject_device(ctx, n, dmap, st, fs, W, H, Q, xyzw, xs, xfs));
 }
 
 // [Utility::dmap2pcl] src/utility.cpp:242-262
@@ -596,7 +611,7 @@ int mvsv_remap_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_
         ss < (size_t)sw || ds < (size_t)dw || ms < (size_t)dw)
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad remap arguments");
     DeviceGuard dev_guard(ctx->device);
-    return remap_device(ctx, n, src, ss, sfs, sw, sh, mx, my, ms, dst, ds, dfs, dw, dh);
+    return mark_last_use(ctx, remap_device(ctx, n, src, ss, sfs, sw, sh, mx, my, ms, dst, ds, dfs, dw, dh));
 }
 
 // [Stereosystem::getRectifiedImagepair] src/Stereosystem.cpp:243-262

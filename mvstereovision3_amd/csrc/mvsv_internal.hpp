@@ -102,7 +102,12 @@ struct mvsv_ctx {
     int* report = nullptr;      // host view
     int* report_dev = nullptr;  // device view of report
     int* report_target = nullptr;
-    hipEvent_t ev_switch = nullptr;  // orders a new stream after the previous one
+    // context-owned "last use" event: recorded on ctx->stream at the end of every
+    // enqueueing entry point; a stream switch makes the new stream wait on it
+    // (never records on the previous stream handle, which the caller may have
+    // destroyed since)
+    hipEvent_t ev_last = nullptr;
+    bool last_valid = false;
     hipStream_t aux = nullptr;  // second stream for concurrent direction passes
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int path16 = 1;  // 16-lanes-per-scanline path kernels where D allows
@@ -139,6 +144,9 @@ int check_hip(mvsv_ctx* ctx, hipError_t e, const char* what);
 int check_report(mvsv_ctx* ctx);
 // Host-mapped int (host and device views), zeroed.
 int alloc_report(mvsv_ctx* ctx, int count, int** host, int** dev);
+// Records the context's last-use event on ctx->stream after an entry point
+// enqueued work (keeps rc: an error code passes through unchanged).
+int mark_last_use(mvsv_ctx* ctx, int rc);
 
 enum Stage {
     kStagePre = 0,

@@ -2728,7 +2728,7 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
             // 640x480 frame 0.097 -> 0.073 ms, two 0.124 -> 0.110 ms, one
             // 1280x960 frame 0.227 -> 0.187 ms
             long best = -1;
-            for (int ty : {120, 96, 64, 48, 32, 24, 16}) {
+            for (int ty : kCostTileHeights) {
                 const long per_cu = (tiles(ty) + ctx->cus - 1) / ctx->cus;
                 const long c = per_cu * (ty + 2 * e.SH2) * (per_cu == 1 ? 3 : 2);
                 if (best < 0 || c < best) {

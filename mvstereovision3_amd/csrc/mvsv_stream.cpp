@@ -161,7 +161,8 @@ static int stream_launch(mvsv_stream* st)
             status = mean_grid_device(ctx, n, first.dOut + (size_t)q.y0 * W + q.x0, W, px, q.x1 - q.x0,
                                       q.y1 - q.y0, first.dMeans);
         }
-        if ((rc = check_hip(ctx, hipEventRecord(last.computed, ctx->stream), "stream event")) ||
+        if ((rc = mark_last_use(ctx, MVSV_OK)) ||
+            (rc = check_hip(ctx, hipEventRecord(last.computed, ctx->stream), "stream event")) ||
             (rc = check_hip(ctx, hipStreamWaitEvent(st->down, last.computed, 0), "stream wait")))
             return rc;
         for (int k = 0; k < n; k++) {
@@ -253,7 +254,7 @@ int mvsv_stream_pop(mvsv_stream* st, int16_t* out, size_t os, float* means)
     st->tail++;
     if (rc) return rc;
     if (s.run_len > 0) {  // first frame of its launch: that launch has completed
-        const bool gave_up = __atomic_load_n(&st->rep[idx], __ATOMIC_ACQUIRE) != 0;
+        const bool gave_up = __atomic_exchange_n(&st->rep[idx], 0, __ATOMIC_ACQ_REL) != 0;
         for (int k = 0; k < s.run_len; k++) st->slots[idx + k].gave_up = gave_up;
         s.run_len = 0;
     }

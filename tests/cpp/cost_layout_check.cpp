@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <iterator>
 #include <vector>
 
 #include "../../mvstereovision3_amd/csrc/mvsv_cost_layout.hpp"
@@ -143,7 +144,10 @@ int main()
     const int widths[] = {23, 360, 641, 1280};
     const int heights[] = {1, 5, 80, 960};
     const int mins[] = {-3, 0, 1};
-    const int tys[] = {1, 16, 48, 120};
+    // every height the launcher picks (kCostTileHeights) plus 1 (a forced
+    // MVSV_COST_TY extreme)
+    std::vector<int> tys(std::begin(kCostTileHeights), std::end(kCostTileHeights));
+    tys.push_back(1);
     for (int D = 16; D <= 512; D += 16)
         for (int SW2 = 0; SW2 <= 7; SW2++)
             for (int TY : tys) {

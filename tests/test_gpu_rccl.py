@@ -57,3 +57,25 @@ def test_rccl_gather_one_rank(gpu, mvsv, oracle, tmp_path):
     for i in range(2):
         L, R = mvsv.synth_pair(0x5EED0000 + i, 200, 96, 1, 64)
         assert np.array_equal(maps[i], oracle.sgbm(L, R, p)), f"frame {i}"
+
+
+def test_bench_force_gather_one_rank(gpu, tmp_path):
+    """bench.py --force-gather: the code path of the driver's 8-GPU run (a
+    torch.distributed.run child, an NCCL process group, dist.gather of the maps
+    inside the timed steps, max-over-ranks wall time) on one rank, with the
+    gathered frames checked against the oracle on rank 0."""
+    import json
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--force-gather",
+           "--steps", "3", "--warmup", "1", "--frames", "2", "--width", "640", "--height", "480",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 1
+    assert res["config"]["gather"] == "rccl"
+    assert res["config"]["launch"] == "torch.distributed.run"
+    assert res["parity_sample_gathered"].startswith("1/1 "), res["parity_sample_gathered"]
+    assert res["value"] > 0
