@@ -276,6 +276,21 @@ MVSV_API int mvsv_rectify_pair(mvsv_ctx* ctx, const uint8_t* left, size_t left_s
                                const float* const* maps, const mvsv_rect* roi, uint8_t* out_left,
                                size_t out_left_stride, uint8_t* out_right, size_t out_right_stride);
 
+/* cv::resize(src, dst, Size(0, 0), fx, fy, INTER_LINEAR) for CV_8UC1 -- the resize
+ * step of Stereosystem::getRectifiedImagepair(Stereopair&, float)
+ * (src/Stereosystem.cpp:279-315), in OpenCV 3.4's arithmetic (11-bit fixed-point
+ * taps; a factor of exactly 0.5 takes INTER_AREA's fast 2x2 path).
+ * mvsv_resize_size: the output size (cvRound(width * fx), cvRound(height * fy)).
+ * mvsv_resize_device: n frames, device pointers, strides in bytes.
+ * mvsv_resize: one host image (dst holds the mvsv_resize_size image). */
+MVSV_API int mvsv_resize_size(int src_width, int src_height, double fx, double fy, int* dst_width,
+                              int* dst_height);
+MVSV_API int mvsv_resize_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t src_stride,
+                                size_t src_frame_stride, int src_width, int src_height, double fx,
+                                double fy, uint8_t* dst, size_t dst_stride, size_t dst_frame_stride);
+MVSV_API int mvsv_resize(mvsv_ctx* ctx, const uint8_t* src, size_t src_stride, int src_width,
+                         int src_height, double fx, double fy, uint8_t* dst, size_t dst_stride);
+
 /* cv::initUndistortRectifyMap(K, dist, R, P, size, CV_32FC1): K 3x3, dist =
  * (k1, k2, p1, p2[, k3[, k4, k5, k6]]) with ndist in {0, 4, 5, 8}, R 3x3, P 3x3 or
  * the left 3x3 of a 3x4 projection (row-major doubles).  Double-precision

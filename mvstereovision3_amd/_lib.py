@@ -140,6 +140,10 @@ def _declare(lib, strict=True):
         "mvsv_remap_device": ([P, I, P, Z, Z, I, I, P, P, Z, P, Z, Z, I, I], I),
         "mvsv_rectify_pair": ([P, P, Z, P, Z, I, I, P, P, P, Z, P, Z], I),
         "mvsv_init_undistort_rectify_map": ([P, P, I, P, P, I, I, P, P, Z], I),
+        "mvsv_resize_size": ([I, I, ctypes.c_double, ctypes.c_double, ctypes.POINTER(I),
+                              ctypes.POINTER(I)], I),
+        "mvsv_resize_device": ([P, I, P, Z, Z, I, I, ctypes.c_double, ctypes.c_double, P, Z, Z], I),
+        "mvsv_resize": ([P, P, Z, I, I, ctypes.c_double, ctypes.c_double, P, Z], I),
         "mvsv_reproject_device": ([P, I, P, Z, Z, I, I, P, P, Z, Z], I),
         "mvsv_calc_coordinate": ([ctypes.c_float] * 3 + [P, P], None),
         "mvsv_calc_distance": ([ctypes.c_float] * 3 + [P], ctypes.c_float),

@@ -246,11 +246,19 @@ class Stereosystem:
     def resetRectification(self):
         self.mIsInit = False
 
-    def getRectifiedImagepair(self, sip) -> bool:
-        """Remap sip.mLeft / sip.mRight (the raw pair) on the GPU and crop to the display ROI."""
-        from .rectify import rectify_pair
+    def getRectifiedImagepair(self, sip, factor=None) -> bool:
+        """Remap sip.mLeft / sip.mRight (the raw pair) on the GPU and crop to the
+        display ROI; with ``factor`` (the (Stereopair&, float) overload,
+        src/Stereosystem.cpp:279-315) the cropped pair is then cv::resize'd by
+        it -- only when the rectification was already initialised: the
+        reference's first call (which initialises) returns the unresized crop."""
+        from .rectify import rectify_pair, resize
+        was_init = self.mIsInit
         if not self.mIsInit and not self.initRectification():
             return False
         maps = (self.mMap1[0], self.mMap2[0], self.mMap1[1], self.mMap2[1])
         sip.mLeft, sip.mRight = rectify_pair(sip.mLeft, sip.mRight, maps, self.mDisplayROI)
+        if factor is not None and was_init:
+            f = float(np.float32(factor))  # the reference's float parameter
+            sip.mLeft, sip.mRight = resize(sip.mLeft, f, f), resize(sip.mRight, f, f)
         return True

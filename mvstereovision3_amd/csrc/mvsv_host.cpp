@@ -276,6 +276,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
     if (const char* v = std::getenv("MVSV_COST_TY")) c->cost_ty = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("MVSV_PATH_SCHEDULE")) c->path_sched = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("MVSV_STRIP_WAVES")) c->strip_waves = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("MVSV_STRIP_LPC")) c->strip_lpc = std::atoi(v) == 8 ? 8 : 16;
     if (const char* v = std::getenv("MVSV_BM_TY")) c->bm_ty = std::max(0, std::min(128, std::atoi(v)));
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess) {
         (void)hipGetLastError();
@@ -612,6 +613,49 @@ int mvsv_remap_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad remap arguments");
     DeviceGuard dev_guard(ctx->device);
     return mark_last_use(ctx, remap_device(ctx, n, src, ss, sfs, sw, sh, mx, my, ms, dst, ds, dfs, dw, dh));
+}
+
+int mvsv_resize_size(int sw, int sh, double fx, double fy, int* dw, int* dh)
+{
+    if (!dw || !dh) return MVSV_E_INVALID_ARG;
+    return resize_size(sw, sh, fx, fy, dw, dh);
+}
+
+// [cv::resize in Stereosystem::getRectifiedImagepair(Stereopair&, float)] src/Stereosystem.cpp:279-315
+int mvsv_resize_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_t sfs, int sw, int sh,
+                       double fx, double fy, uint8_t* dst, size_t ds, size_t dfs)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    int dw, dh;
+    if (n <= 0 || !src || !dst || ss < (size_t)std::max(sw, 0) || resize_size(sw, sh, fx, fy, &dw, &dh))
+        return set_error(ctx, MVSV_E_INVALID_ARG, "bad resize arguments");
+    DeviceGuard dev_guard(ctx->device);
+    return mark_last_use(ctx, resize_device(ctx, n, src, ss, sfs, sw, sh, fx, fy, dst, ds, dfs));
+}
+
+int mvsv_resize(mvsv_ctx* ctx, const uint8_t* src, size_t ss, int sw, int sh, double fx, double fy,
+                uint8_t* dst, size_t ds)
+{
+    if (!ctx) return MVSV_E_INVALID_ARG;
+    int dw, dh;
+    if (!src || !dst || ss < (size_t)std::max(sw, 0) || resize_size(sw, sh, fx, fy, &dw, &dh) ||
+        ds < (size_t)dw)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "bad resize arguments");
+    DeviceGuard dev_guard(ctx->device);
+    const size_t in = (size_t)sw * sh, outb = (size_t)dw * dh;
+    int rc;
+    if ((rc = ensure(ctx, ctx->h_left, in, "resize staging")) ||
+        (rc = ensure(ctx, ctx->h_right, outb, "resize staging")))
+        return rc;
+    hipStream_t s = ctx->stream;
+    if ((rc = check_hip(ctx, hipMemcpy2DAsync(ctx->h_left.ptr, sw, src, ss, sw, sh, hipMemcpyHostToDevice, s),
+                        "H2D image")) ||
+        (rc = resize_device(ctx, 1, (const uint8_t*)ctx->h_left.ptr, sw, in, sw, sh, fx, fy,
+                            (uint8_t*)ctx->h_right.ptr, dw, outb)) ||
+        (rc = check_hip(ctx, hipMemcpy2DAsync(dst, ds, ctx->h_right.ptr, dw, dw, dh, hipMemcpyDeviceToHost, s),
+                        "D2H image")))
+        return rc;
+    return check_hip(ctx, hipStreamSynchronize(s), "hipStreamSynchronize");
 }
 
 // [Stereosystem::getRectifiedImagepair] src/Stereosystem.cpp:243-262

@@ -116,6 +116,7 @@ struct mvsv_ctx {
     int tri = 1;     // sheared-strip kernels: three directions per sweep
     int path_sched = 0;   // 16-lane path schedule: 0 = by launch size, 1 = strips, 2 = directions side by side
     int strip_waves = 0;  // compute waves per strip (0 = by launch size; 4 or the wide count forces)
+    int strip_lpc = 16;   // lanes per strip column for D = 128: 16, or 8 (16 disparities per lane)
     int lines_aux = -1;  // L->R line kernel beside the strip kernel: -1 = small launches only, 0 / 1 / 2 force
     int bm2 = 1;     // StereoBM: disparities-on-lanes match kernel where blockSize <= 21, D <= 128
     int bm_ty = 0;   // its tile height (0 = chosen per launch); MVSV_BM_TY for A/B runs
@@ -190,6 +191,10 @@ int speckle_device(mvsv_ctx* ctx, int n, int16_t* img, size_t st, size_t fs, int
 int remap_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_t sfs, int sw, int sh,
                  const float* mx, const float* my, size_t ms, uint8_t* dst, size_t ds, size_t dfs,
                  int dw, int dh);
+// cv::resize INTER_LINEAR (CV_8UC1) output size / launch (mvsv_post.hip)
+int resize_size(int sw, int sh, double fx, double fy, int* dw, int* dh);
+int resize_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_t sfs, int sw, int sh, double fx,
+                  double fy, uint8_t* dst, size_t ds, size_t dfs);
 int reproject_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_t fs, int W, int H,
                      const float* Q, float* out, size_t os, size_t ofs);
 int mean_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_t fs, int W,

@@ -8,6 +8,9 @@
 //     yields exactly the same components as OpenCV's raster-order flood fill.
 //   * MeanDisparityDetection grid   (src/MeanDisparityDetection.cpp:159-206,
 //     Utility::calcMeanDisparity src/utility.cpp:265-285)
+#include <cfloat>
+#include <cmath>
+
 #include "mvsv_device.hpp"
 #include "mvsv_internal.hpp"
 
@@ -403,6 +406,78 @@ __global__ __launch_bounds__(256) void remap_linear_kernel(
     dst[f * dfs + (size_t)y * ds + x] = (uint8_t)v;
 }
 
+// ---- cv::resize(src, dst, Size(0, 0), fx, fy, INTER_LINEAR), CV_8UC1 ----------
+// The resize of Stereosystem::getRectifiedImagepair(Stereopair&, float)
+// (src/Stereosystem.cpp:279-315).  [OpenCV 3.4 resize.cpp, x86 build] (oracle:
+// orc_resize_linear): x / y source taps and 11-bit coefficients per output
+// column / row in float (fx = (float)((dx + 0.5) * scale - 0.5), sx = floor,
+// coefficients cvRound((1 - f) * 2048), cvRound(f * 2048); x clamped with
+// f = 0, rows clamped); horizontal taps exact in int32; vertical combine as
+// the SIMD op for columns x < simd_end ((S >> 4) x beta >> 16 per row, int16
+// saturating add, (+2) >> 2) and (sum + 2^21) >> 22 past it.  A 2 x 2
+// reduction (scale exactly 2) is INTER_AREA's fast path: (a+b+c+d+2) >> 2 on
+// whole blocks, a float mean rounded half to even on clipped edge blocks.
+__device__ __forceinline__ int sat16(int v) { return clampi(v, -32768, 32767); }
+
+__global__ __launch_bounds__(256) void resize_linear_kernel(const uint8_t* __restrict__ src, size_t ss,
+                                                            size_t sfs, int sw, int sh, double scale_x,
+                                                            double scale_y, int area2, int simd_end,
+                                                            uint8_t* __restrict__ dst, size_t ds, size_t dfs,
+                                                            int dw, int dh)
+{
+    const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.z;
+    if (dx >= dw || dy >= dh) return;
+    const uint8_t* S = src + f * sfs;
+    int v;
+    if (area2) {
+        const int sy0 = 2 * dy, sx0 = 2 * dx;
+        const int w1 = sw / 2;
+        const int w = sy0 + 2 <= sh ? w1 : 0;
+        if (sy0 >= sh || sx0 >= sw) {
+            v = 0;
+        } else if (dx < w) {
+            const uint8_t* r = S + (size_t)sy0 * ss + sx0;
+            v = (r[0] + r[1] + r[ss] + r[ss + 1] + 2) >> 2;
+        } else {
+            int sum = 0, cnt = 0;
+            for (int yy = 0; yy < 2 && sy0 + yy < sh; yy++)
+                for (int xx = 0; xx < 2 && sx0 + xx < sw; xx++) {
+                    sum += S[(size_t)(sy0 + yy) * ss + sx0 + xx];
+                    cnt++;
+                }
+            v = clampi(__float2int_rn((float)sum / (float)cnt), 0, 255);
+        }
+    } else {
+        float fxv = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)floorf(fxv);
+        fxv -= (float)sx;
+        if (sx < 0) fxv = 0.f, sx = 0;
+        if (sx >= sw - 1) fxv = 0.f, sx = sw - 1;
+        const int a0 = __float2int_rn((1.f - fxv) * 2048.f), a1 = __float2int_rn(fxv * 2048.f);
+        float fyv = (float)((dy + 0.5) * scale_y - 0.5);
+        const int sy = (int)floorf(fyv);
+        fyv -= (float)sy;
+        const int b0 = (int)(short)__float2int_rn((1.f - fyv) * 2048.f);
+        const int b1 = (int)(short)__float2int_rn(fyv * 2048.f);
+        const int r0 = clampi(sy, 0, sh - 1), r1 = clampi(sy + 1, 0, sh - 1);
+        const uint8_t* p0 = S + (size_t)r0 * ss + sx;
+        const uint8_t* p1 = S + (size_t)r1 * ss + sx;
+        const int s0 = p0[0] * a0 + (a1 ? p0[1] * a1 : 0);
+        const int s1 = p1[0] * a0 + (a1 ? p1[1] * a1 : 0);
+        if (dx < simd_end) {
+            const int h0 = sat16(s0 >> 4), h1 = sat16(s1 >> 4);
+            const int r = sat16(((h0 * b0) >> 16) + ((h1 * b1) >> 16));
+            v = sat16(r + 2) >> 2;
+        } else {
+            v = (s0 * b0 + s1 * b1 + (1 << 21)) >> 22;
+        }
+        v = clampi(v, 0, 255);
+    }
+    dst[f * dfs + (size_t)dy * ds + dx] = (uint8_t)v;
+}
+
 // ---- Utility::calcCoordinate per pixel (src/utility.cpp:176-198) -------------
 // (X, Y, Z, W) = Q * (x, y, v / 16, 1) with OpenCV's float GEMM (products and
 // sums in double, one rounding to float per element), then Mat /= W as
@@ -491,6 +566,36 @@ int remap_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_t sfs
     hipLaunchKernelGGL(remap_linear_kernel, grid, dim3(256), 0, ctx->stream, src, ss, sfs, sw, sh,
                        mx, my, ms, dst, ds, dfs, dw, dh);
     return check_hip(ctx, hipGetLastError(), "remap");
+}
+
+int resize_size(int sw, int sh, double fx, double fy, int* dw, int* dh)
+{
+    if (sw <= 0 || sh <= 0 || !(fx > 0) || !(fy > 0)) return MVSV_E_INVALID_ARG;
+    const double w = std::nearbyint(sw * fx), h = std::nearbyint(sh * fy);  // cvRound (half to even)
+    if (!(w >= 1 && h >= 1 && w <= 1 << 20 && h <= 1 << 20)) return MVSV_E_INVALID_ARG;
+    *dw = (int)w;
+    *dh = (int)h;
+    return MVSV_OK;
+}
+
+int resize_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_t sfs, int sw, int sh, double fx,
+                  double fy, uint8_t* dst, size_t ds, size_t dfs)
+{
+    int dw, dh;
+    if (resize_size(sw, sh, fx, fy, &dw, &dh)) return set_error(ctx, MVSV_E_INVALID_ARG, "bad resize factors");
+    if (ds < (size_t)dw) return set_error(ctx, MVSV_E_INVALID_ARG, "resize destination stride smaller than width");
+    const double scale_x = 1.0 / fx, scale_y = 1.0 / fy;
+    const double isx = std::nearbyint(scale_x), isy = std::nearbyint(scale_y);
+    const bool area2 = std::fabs(scale_x - isx) < DBL_EPSILON && std::fabs(scale_y - isy) < DBL_EPSILON &&
+                       isx == 2.0 && isy == 2.0;
+    // columns the SIMD vertical op covers: its 16-wide loop, then its 8-wide one
+    int simd_end = 0;
+    while (simd_end <= dw - 16) simd_end += 16;
+    while (simd_end < dw - 8) simd_end += 8;
+    dim3 grid((dw + 63) / 64, (dh + 3) / 4, n);
+    hipLaunchKernelGGL(resize_linear_kernel, grid, dim3(256), 0, ctx->stream, src, ss, sfs, sw, sh, scale_x,
+                       scale_y, area2 ? 1 : 0, simd_end, dst, ds, dfs, dw, dh);
+    return check_hip(ctx, hipGetLastError(), "resize");
 }
 
 int reproject_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_t fs, int W, int H,

@@ -1064,19 +1064,22 @@ __device__ __forceinline__ uint32_t sgm_delta2(int minp, int P2)
 {
     return NW ? (uint32_t)(minp + P2) * 0x10001u : (uint32_t)((minp + P2) & 0xffff) * 0x10001u;
 }
-template <int NP, bool NW = false>
+template <int NP, bool NW = false, int LPC = 16>
 __device__ __forceinline__ void sgm_step_row_t(const uint32_t (&lp)[NP], uint32_t delta2,
                                                uint32_t p1x2, const uint32_t (&c)[NP],
                                                uint32_t (&ln)[NP], uint32_t (&t)[NP])
 {
+    static_assert(LPC == 8 || LPC == 16, "row-DPP segments of 8 or 16 lanes");
     const uint32_t MAXP = 0x7fff7fffu;
     // d-1 / d+1 neighbours across the lane boundary: zero-filled DPP shifts
-    // (bound_ctrl) OR'ed with MAX at the row ends fold into v_or_b32_dpp
-    const uint32_t rl16 = __lane_id() & 15;
+    // (bound_ctrl) OR'ed with MAX at the segment ends fold into v_or_b32_dpp
+    // (an 8-lane segment's first lane receives the previous segment's last
+    // lane; the OR with MAX discards it: L values are in [0, 0x7fff])
+    const uint32_t rls = __lane_id() % LPC;
     const uint32_t prev_hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)lp[NP - 1], 0x111, 0xf, 0xf, true) |
-                             (rl16 == 0 ? MAXP : 0u);
+                             (rls == 0 ? MAXP : 0u);
     const uint32_t next_lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)lp[0], 0x101, 0xf, 0xf, true) |
-                             (rl16 == 15 ? MAXP : 0u);
+                             (rls == LPC - 1 ? MAXP : 0u);
     uint32_t X[NP + 1];  // X[q + 1] = X_q, X[0] = X_{-1}
     X[0] = pk_min(prev_hi, lp[0]);
 #pragma unroll
@@ -1085,6 +1088,33 @@ __device__ __forceinline__ void sgm_step_row_t(const uint32_t (&lp)[NP], uint32_
 #pragma unroll
     for (int p = 0; p < NP; p++)
         sgm_pair<NW>(lp[p], __builtin_amdgcn_alignbit(X[p + 1], X[p], 16), delta2, p1x2, c[p], ln[p], t[p]);
+}
+
+// Minimum over an LPC-lane segment (8: one half of a DPP row, 16: a row);
+// every lane of the segment gets it.
+template <int LPC>
+__device__ __forceinline__ int seg_lane_min(int v)
+{
+    static_assert(LPC == 8 || LPC == 16, "row-DPP segments of 8 or 16 lanes");
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true));   // quad_perm [1,0,3,2]
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true));   // quad_perm [2,3,0,1]
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, true));  // row_half_mirror
+    if constexpr (LPC == 16) v = min(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, true));  // row_mirror
+    return v;
+}
+
+// The lane's minimum over its NP pairs in BOTH halves (the swap is a VOP3P
+// op_sel, no extra instruction): for L in [0, 0x7fff] the packed (m, m) orders
+// like m as an int32, so the segment butterfly runs on it unchanged and the
+// next step's packed delta = (minLp + P2) x 2 is one v_add_u32 (no-wrap form).
+template <int NP>
+__device__ __forceinline__ uint32_t lane_min_pk(const uint32_t (&ln)[NP])
+{
+    uint32_t m = ln[0];
+#pragma unroll
+    for (int p = 1; p < NP; p++) m = pk_min(m, ln[p]);
+    const s16x2 v = as_s2(m);
+    return as_u(__builtin_elementwise_min(v, __builtin_shufflevector(v, v, 1, 0)));
 }
 
 template <int NP>
@@ -1241,39 +1271,54 @@ __global__ __launch_bounds__(256) void sgbm_pathdirs16_kernel(const int16_t* __r
 // strips, 8 (4 for D = 256) compute waves -- the latency shape for one or two
 // frames, where wide strips leave most CUs idle and each step of a strip is
 // the serial work of its CU (see launch_tri)
-template <int NP>
-constexpr int tri_wide_waves() { return NP >= 8 ? 7 : 15; }
-template <int NP>
-constexpr int tri_narrow_waves() { return NP >= 8 ? 4 : 8; }
-template <int NP, int WV>
+// LPC = lanes per U-column (2*NP disparities each, D = 2*NP*LPC): 16 (one DPP
+// row per column) or 8 (half a DPP row, twice the disparities per lane: the
+// per-column minimum is a 3-step butterfly, and the lane-boundary neighbours,
+// the step's row minima and its bookkeeping are shared by twice the work --
+// the throughput shape for D = 128 batches, two 512-thread blocks per CU).
+template <int NP, int LPC = 16>
+constexpr int tri_wide_waves() { return LPC == 8 ? 7 : (NP >= 8 ? 7 : 15); }
+template <int NP, int LPC = 16>
+constexpr int tri_narrow_waves() { return LPC == 8 ? 4 : (NP >= 8 ? 4 : 8); }
+template <int NP, int WV, int LPC = 16>
 struct TriCfg {
     static constexpr int kWaves = WV;
-    static constexpr int kSW = 4 * kWaves;  // U-columns per strip
+    static constexpr int kCPW = 64 / LPC;   // U-columns per compute wave
+    static constexpr int kSW = kCPW * kWaves;  // U-columns per strip
     static constexpr int kThreads = 64 * (kWaves + 1);
+    // blocks per CU the register budget aims at: one 1024-thread block, or two
+    // 512-thread ones (4 waves per SIMD either way); D = 256 on 16 lanes: 2
+    static constexpr int kWavesPerEU = (NP >= 8 && LPC == 16) ? 2 : 4;
 };
 #ifndef MVSV_TRI_PF
 #define MVSV_TRI_PF 4
+#endif
+#ifndef MVSV_TRI_STEP_SEQ
+#define MVSV_TRI_STEP_SEQ 0  // 1: the three recurrences of a step one after the other (A/B)
 #endif
 constexpr int kTriPF = MVSV_TRI_PF;     // steps of C prefetch (compute waves)
 constexpr int kTriBF = 4;               // steps of boundary prefetch (comm wave)
 constexpr int kTriUnroll = 4;           // lcm(kTriPF, kTriBF, 2)
 
-template <int NP, int WV>
+template <int NP, int WV, int LPC = 16>
 struct TriLayout {
-    static constexpr int kCols = TriCfg<NP, WV>::kSW + 2;  // + two columns of the right strip
-    // dwords per column, odd: lane (column c, rl) reads / writes element p of
-    // its 2*NP disparities at c*kColDw + rl*NP + p, so for NP = 4 the 64 lanes
-    // of one b32 access hit 64 distinct banks (c + 4 rl + p mod 64); with the
-    // unpadded 16*NP stride the wave's 4 columns aliased onto the same 16
-    // banks (4-way conflicts on every neighbour read after the step barrier)
-    static constexpr int kColDw = 16 * NP + 1;
+    static constexpr int kCols = TriCfg<NP, WV, LPC>::kSW + 2;  // + two columns of the right strip
+    // Element-major columns: lane (column c, rl) keeps element p of its 2*NP
+    // disparities at c*kColDw + p*LPC + rl.  A b32 access (ds_read2_b32 /
+    // ds_write2_b32) is served per 32-lane half-wave on 32 banks ((a/4) mod 32,
+    // MI355X_MICROARCH.md §LDS); the half-wave holds 32/LPC columns, and with
+    // kColDw = LPC (mod 32) they land on disjoint bank ranges: conflict-free.
+    // (The former lane-major layout, c*kColDw + rl*NP + p with an odd stride,
+    // mapped lanes rl and rl + 32/NP of a column onto one bank: 2-way
+    // conflicts, SQ_LDS_BANK_CONFLICT 44 % of the LDS cycles.)
+    static constexpr int kColDw = ((NP * LPC + 31) / 32) * 32 + LPC % 32;
     static constexpr int kBufDw = 2 * kCols * kColDw;   // dirs b and c
     static constexpr int kLDw = 2 * kBufDw;             // double-buffered
     static constexpr int kMinInts = 2 * 2 * kCols;      // [buf][dir][col]
     static constexpr size_t kBytes = (size_t)(kLDw + kMinInts) * 4;
 };
 
-// Boundary granules of one strip and step: [NG][4 item rows][16 lanes] u64
+// Boundary granules of one strip and step: [NG][4 item rows][LPC lanes] u64
 // (the 4th item row is never written: the comm wave's spare lanes repeat
 // item 2).  Item 0 = L of dir
 // (0, sy) at the strip's first column, 1 = dir (-1, sy) at the first column,
@@ -1315,27 +1360,28 @@ struct TriGran {
     }
 };
 
-template <int NP>
+template <int NP, int LPC = 16>
 __device__ __forceinline__ size_t tri_slot(int chain, int k, int t, int nchains, int H)
 {
-    return ((((size_t)k * nchains + chain) * H + t) * 4) * 16 * TriGran<NP>::NG;
+    return ((((size_t)k * nchains + chain) * H + t) * 4) * LPC * TriGran<NP>::NG;
 }
 
-template <int NP, int WV, typename AccT, bool NW = false>
-__global__ __launch_bounds__((TriCfg<NP, WV>::kThreads))
-__attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
+template <int NP, int WV, int LPC, typename AccT, bool NW = false>
+__global__ __launch_bounds__((TriCfg<NP, WV, LPC>::kThreads))
+__attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm_tri_kernel(
     const int16_t* __restrict__ C, AccT* __restrict__ A, size_t plane, AccT* __restrict__ dummy,
     int H, int W1, int D, int npass, int P1, int P2, unsigned long long* __restrict__ bnd,
     unsigned epoch, int nframes, int nstrips, int* __restrict__ status, unsigned spin_limit,
     int* __restrict__ report, unsigned long long* __restrict__ stats)
 {
     using AV = AccVec<NP, AccT>;
-    using TL = TriLayout<NP, WV>;
+    using TL = TriLayout<NP, WV, LPC>;
     using TG = TriGran<NP>;
     constexpr int NG = TG::NG;
-    constexpr int kTriWaves = TriCfg<NP, WV>::kWaves;
-    constexpr int kTriSW = TriCfg<NP, WV>::kSW;
-    constexpr int PF = NP >= 8 ? 2 : kTriPF;  // D = 256: 256 VGPRs already
+    constexpr int kTriWaves = TriCfg<NP, WV, LPC>::kWaves;
+    constexpr int kTriSW = TriCfg<NP, WV, LPC>::kSW;
+    constexpr int kCPW = TriCfg<NP, WV, LPC>::kCPW;
+    constexpr int PF = NP >= 8 ? 2 : kTriPF;  // 16 disparities per lane: registers
     constexpr int BF = kTriBF;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* lds = (uint32_t*)smem;
@@ -1343,7 +1389,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool comm = w == kTriWaves;
-    const int r = lane >> 4, rl = lane & 15;
+    const int r = lane / LPC, rl = lane % LPC;
     // strips counted from the right; passes and frames interleaved, so every
     // block's producer (same pass and frame, strip k-1) has a lower index.
     // Pass 0 sweeps down (sy = +1), pass 1 up (sy = -1), each into its own
@@ -1357,7 +1403,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     A = acc_add(A, (ptrdiff_t)pass * (ptrdiff_t)plane);
     const int Utot = W1 + H - 1;
     const int U0 = Utot - kTriSW * (k + 1);
-    const int col = 4 * w + r;  // compute waves
+    const int col = kCPW * w + r;  // compute waves
     const int U = U0 + col;
     // active steps: some column of the strip has 0 <= x = U - (H-1) + t < W1
     const int tb = max(0, (H - 1) - (U0 + kTriSW - 1));
@@ -1375,7 +1421,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     const unsigned long long tag = (unsigned long long)tag16 << 48;
 
     auto lcol = [&](int buf, int dir, int c) -> uint32_t* {
-        return lds + (size_t)((buf * 2 + dir) * TL::kCols + c) * TL::kColDw + rl * NP;
+        return lds + (size_t)((buf * 2 + dir) * TL::kCols + c) * TL::kColDw + rl;  // element p at [p * LPC]
     };
     auto mcol = [&](int buf, int dir, int c) -> int* { return lmin + (buf * 2 + dir) * TL::kCols + c; };
 
@@ -1393,10 +1439,10 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     const int bcol = kTriSW + (jj == 2 ? 1 : 0);  // LDS column the consumed item lands in
     const int bdir = jj == 0 ? 0 : 1;
     const int pcol = jj == 2 ? 1 : 0;              // own column published as item jj
-    const size_t bstep = (size_t)4 * 16 * NG;
+    const size_t bstep = (size_t)4 * LPC * NG;
     const unsigned long long* bsrc =
-        bnd + tri_slot<NP>(chain, k > 0 ? k - 1 : k, 0, nchains, H) + (size_t)jj * 16 + rl;
-    unsigned long long* pdst = bnd + tri_slot<NP>(chain, k, 0, nchains, H) + (size_t)jj * 16 + rl;
+        bnd + tri_slot<NP, LPC>(chain, k > 0 ? k - 1 : k, 0, nchains, H) + (size_t)jj * LPC + rl;
+    unsigned long long* pdst = bnd + tri_slot<NP, LPC>(chain, k, 0, nchains, H) + (size_t)jj * LPC + rl;
     auto bvalid = [&](int t) {
         const int xx = U0 + bcol - (H - 1) + t;
         return k > 0 && t >= 0 && xx >= 0 && xx < W1;
@@ -1404,7 +1450,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
     auto bload = [&](int t, unsigned long long (&g)[NG]) {
         const unsigned long long* q = bsrc + (size_t)clampi(t, 0, H - 1) * bstep;
 #pragma unroll
-        for (int i = 0; i < NG; i++) g[i] = __hip_atomic_load(q + 64 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 0; i < NG; i++) g[i] = __hip_atomic_load(q + 4 * LPC * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     // item t into LDS row buf, spinning until the producer's tag shows
     auto bconsume = [&](int t, int buf, unsigned long long (&g)[NG]) {
@@ -1435,7 +1481,7 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
                 ok = true;
 #pragma unroll
                 for (int i = 0; i < NG; i++) {
-                    g[i] = __hip_atomic_load(q + 64 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    g[i] = __hip_atomic_load(q + 4 * LPC * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     ok &= !need || (unsigned)(g[i] >> 48) == tag16;
                 }
             }
@@ -1450,8 +1496,9 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
         if (jlive) {
             uint32_t* dst = lcol(buf, bdir, bcol);
 #pragma unroll
-            for (int i = 0; i < NP; i++) dst[i] = need ? v[i] : 0u;
-            if (rl == 0) *mcol(buf, bdir, bcol) = need ? mn : 0;
+            for (int i = 0; i < NP; i++) dst[i * LPC] = need ? v[i] : 0u;
+            // the compute waves keep column minima packed (m, m) in the no-wrap form
+            if (rl == 0) *mcol(buf, bdir, bcol) = need ? (NW ? (int)((uint32_t)mn * 0x10001u) : mn) : 0;
         }
     };
     // publish step t of this strip's columns 0 and 1 (LDS row buf) for the left
@@ -1460,13 +1507,13 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
         uint32_t v[NP];
         const uint32_t* src = lcol(buf, bdir, pcol);
 #pragma unroll
-        for (int i = 0; i < NP; i++) v[i] = src[i];
+        for (int i = 0; i < NP; i++) v[i] = src[i * LPC];
         const int mn = *mcol(buf, bdir, pcol);
         unsigned long long g[NG];
         TG::pack(v, mn, tag, g);
         unsigned long long* q = pdst + (size_t)clampi(t, 0, H - 1) * bstep;
 #pragma unroll
-        for (int i = 0; i < NG; i++) __hip_atomic_store(q + 64 * i, g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 0; i < NG; i++) __hip_atomic_store(q + 4 * LPC * i, g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
 
     // ---- compute waves ----
@@ -1511,69 +1558,122 @@ __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 2 : 4))) void sgbm_tri_kernel(
         bload(t + BF, bg[j % BF]);
         __syncthreads();
     };
+    // One step: the three recurrences one after the other (each direction's
+    // neighbours, update, column minimum and LDS hand-over before the next
+    // starts, so only one direction's temporaries are live); the output word
+    // accumulates the deltas as they come.
+    const uint32_t p2x2 = (uint32_t)(P2 & 0xffff) * 0x10001u;
     auto step = [&](int i, int j) {
         const int t = tb + i;
         const int cur = i & 1, prv = cur ^ 1;
-        {
-            const int x = cell_x(t);
-            const bool valid = x >= 0 && x < W1;
-            uint32_t c[NP];
+        const int x = cell_x(t);
+        const bool valid = x >= 0 && x < W1;
+        const bool allv = __all(valid);
+        uint32_t c[NP];
 #pragma unroll
-            for (int p = 0; p < NP; p++) c[p] = cb[j % PF].v[p];
-            cb[j % PF].load(Cf + cell_off(min(t + PF, te - 1)));
-            uint32_t pb[NP], pc[NP];
-            {
-                const uint32_t* sb = lcol(prv, 0, col + 1);
-                const uint32_t* sc = lcol(prv, 1, col + 2);
+        for (int p = 0; p < NP; p++) c[p] = cb[j % PF].v[p];
+        cb[j % PF].load(Cf + cell_off(min(t + PF, te - 1)));
+        // the column minimum of one direction (packed (m, m) in the no-wrap
+        // form) and the next step's delta from it
+        auto dmin = [&](const uint32_t (&n)[NP]) -> int {
+            if constexpr (NW)
+                return seg_lane_min<LPC>((int)lane_min_pk<NP>(n));
+            else
+                return seg_lane_min<LPC>(lane_min_row<NP>(n));
+        };
+        auto dl2 = [&](int m) -> uint32_t {
+            if constexpr (NW)
+                return (uint32_t)m + p2x2;  // (minLp + P2) x 2, no carry between halves
+            else
+                return sgm_delta2<false>(m, P2);
+        };
+        // sum of the three deltas t_r + P2 = 3 P2 - (u_a + u_b + u_c) (no-wrap)
+        // or t_a + t_b + t_c + 3 P2, exact in u16 wrap arithmetic
+        auto acc = [&](uint32_t o, uint32_t u) -> uint32_t { return NW ? pk_sub_u16(o, u) : pk_add_u16(o, u); };
+        uint32_t o[NP];
+#if MVSV_TRI_STEP_SEQ
+        {  // (1, sy): the strip's own column, state in registers
+            uint32_t n[NP], u[NP];
+            sgm_step_row_t<NP, NW, LPC>(la, dl2(ma), p1x2, c, n, u);
 #pragma unroll
-                for (int p = 0; p < NP; p++) {
-                    pb[p] = sb[p];
-                    pc[p] = sc[p];
-                }
+            for (int p = 0; p < NP; p++) o[p] = acc(p2x3, u[p]);
+            const int mn = dmin(n);
+            if (__builtin_expect(!allv, 0)) {
+#pragma unroll
+                for (int p = 0; p < NP; p++) n[p] = valid ? n[p] : 0u;
             }
-            const int mb = *mcol(prv, 0, col + 1), mc = *mcol(prv, 1, col + 2);
-            uint32_t na[NP], nb[NP], nc[NP], ta[NP], tb_[NP], tc[NP];
-            sgm_step_row_t<NP, NW>(la, sgm_delta2<NW>(ma, P2), p1x2, c, na, ta);
-            sgm_step_row_t<NP, NW>(pb, sgm_delta2<NW>(mb, P2), p1x2, c, nb, tb_);
-            sgm_step_row_t<NP, NW>(pc, sgm_delta2<NW>(mc, P2), p1x2, c, nc, tc);
-            const int mna = row_min_i32(lane_min_row<NP>(na));
-            // DPP-folded i32 row minima (v_min_i32_dpp): one op per butterfly step
-            const int mnb = row_min_i32(lane_min_row<NP>(nb));
-            const int mnc = row_min_i32(lane_min_row<NP>(nc));
-            uint32_t o[NP];
+#pragma unroll
+            for (int p = 0; p < NP; p++) la[p] = n[p];
+            ma = valid ? mn : 0;
+        }
+#pragma unroll
+        for (int dir = 0; dir < 2; dir++) {  // (0, sy) from column col + 1, (-1, sy) from col + 2
+            uint32_t pv[NP];
+            const uint32_t* src = lcol(prv, dir, col + 1 + dir);
+#pragma unroll
+            for (int p = 0; p < NP; p++) pv[p] = src[p * LPC];
+            const int mp = *mcol(prv, dir, col + 1 + dir);
+            uint32_t n[NP], u[NP];
+            sgm_step_row_t<NP, NW, LPC>(pv, dl2(mp), p1x2, c, n, u);
+#pragma unroll
+            for (int p = 0; p < NP; p++) o[p] = acc(o[p], u[p]);
+            const int mn = dmin(n);
+            if (__builtin_expect(!allv, 0)) {
+#pragma unroll
+                for (int p = 0; p < NP; p++) n[p] = valid ? n[p] : 0u;
+            }
+            uint32_t* dst = lcol(cur, dir, col);
+#pragma unroll
+            for (int p = 0; p < NP; p++) dst[p * LPC] = n[p];
+            if (rl == 0) *mcol(cur, dir, col) = valid ? mn : 0;
+        }
+#else
+        // the three recurrences side by side (the compiler interleaves their
+        // independent chains; measured faster than one after the other)
+        uint32_t pb[NP], pc[NP];
+        {
+            const uint32_t* sb = lcol(prv, 0, col + 1);
+            const uint32_t* sc = lcol(prv, 1, col + 2);
 #pragma unroll
             for (int p = 0; p < NP; p++) {
-                // sum of the three deltas t_r + P2 = 3 P2 - (u_a + u_b + u_c),
-                // exact in u16 wrap arithmetic
-                if constexpr (NW)
-                    o[p] = pk_sub_u16(p2x3, pk_add_u16(pk_add_u16(ta[p], tb_[p]), tc[p]));
-                else
-                    o[p] = pk_add_u16(pk_add_u16(ta[p], tb_[p]), pk_add_u16(tc[p], p2x3));
+                pb[p] = sb[p * LPC];
+                pc[p] = sc[p * LPC];
             }
-            AV::store(valid ? acc_addu(Af, cell_off(t)) : dp, o);
-            if (__builtin_expect(!__all(valid), 0)) {
+        }
+        const int mb = *mcol(prv, 0, col + 1), mc = *mcol(prv, 1, col + 2);
+        uint32_t na[NP], nb[NP], nc[NP], ta[NP], tb_[NP], tc[NP];
+        sgm_step_row_t<NP, NW, LPC>(la, dl2(ma), p1x2, c, na, ta);
+        sgm_step_row_t<NP, NW, LPC>(pb, dl2(mb), p1x2, c, nb, tb_);
+        sgm_step_row_t<NP, NW, LPC>(pc, dl2(mc), p1x2, c, nc, tc);
+        const int mna = dmin(na), mnb = dmin(nb), mnc = dmin(nc);
 #pragma unroll
-                for (int p = 0; p < NP; p++) {
-                    na[p] = valid ? na[p] : 0u;
-                    nb[p] = valid ? nb[p] : 0u;
-                    nc[p] = valid ? nc[p] : 0u;
-                }
+        for (int p = 0; p < NP; p++) o[p] = acc(acc(acc(p2x3, ta[p]), tb_[p]), tc[p]);
+        if (__builtin_expect(!allv, 0)) {
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                na[p] = valid ? na[p] : 0u;
+                nb[p] = valid ? nb[p] : 0u;
+                nc[p] = valid ? nc[p] : 0u;
             }
+        }
 #pragma unroll
-            for (int p = 0; p < NP; p++) la[p] = na[p];
-            ma = valid ? mna : 0;
+        for (int p = 0; p < NP; p++) la[p] = na[p];
+        ma = valid ? mna : 0;
+        {
             uint32_t* db = lcol(cur, 0, col);
             uint32_t* dc = lcol(cur, 1, col);
 #pragma unroll
             for (int p = 0; p < NP; p++) {
-                db[p] = nb[p];
-                dc[p] = nc[p];
+                db[p * LPC] = nb[p];
+                dc[p * LPC] = nc[p];
             }
             if (rl == 0) {
                 *mcol(cur, 0, col) = valid ? mnb : 0;
                 *mcol(cur, 1, col) = valid ? mnc : 0;
             }
         }
+#endif
+        AV::store(valid ? acc_addu(Af, cell_off(t)) : dp, o);
         __syncthreads();
     };
     const int len = te - tb;
@@ -2298,14 +2398,14 @@ static int path_schedule(const mvsv_ctx* ctx, const SgbmEff& e, int H, int n)
     return use_strips(ctx, e, H) ? 1 : 0;
 }
 
-template <int NP, int WV, typename AccT, bool NW>
+template <int NP, int WV, int LPC, typename AccT, bool NW>
 int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
                   int npass)
 {
-    using TL = TriLayout<NP, WV>;
-    constexpr int kTriSW = TriCfg<NP, WV>::kSW;
+    using TL = TriLayout<NP, WV, LPC>;
+    constexpr int kTriSW = TriCfg<NP, WV, LPC>::kSW;
     const int nstrips = (e.W1 + H - 1 + kTriSW - 1) / kTriSW;
-    const size_t bytes = (size_t)npass * n * nstrips * H * 4 * 16 * TriGran<NP>::NG * 8;
+    const size_t bytes = (size_t)npass * n * nstrips * H * 4 * LPC * TriGran<NP>::NG * 8;
     int rc;
     if (ctx->tri_bnd.bytes < bytes) {
         if ((rc = ensure(ctx, ctx->tri_bnd, bytes, "sgbm strip boundary granules"))) return rc;
@@ -2336,7 +2436,12 @@ int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, Ac
         (void)hipMalloc(&stats, (size_t)grid.x * 64);
         (void)hipMemset(stats, 0, (size_t)grid.x * 64);
     }
-    hipLaunchKernelGGL((sgbm_tri_kernel<NP, WV, AccT, NW>), grid, dim3(TriCfg<NP, WV>::kThreads), TL::kBytes,
+    if (TL::kBytes > 65536 &&
+        (rc = check_hip(ctx, hipFuncSetAttribute((const void*)sgbm_tri_kernel<NP, WV, LPC, AccT, NW>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)TL::kBytes),
+                        "sgbm strip LDS attribute")))
+        return rc;
+    hipLaunchKernelGGL((sgbm_tri_kernel<NP, WV, LPC, AccT, NW>), grid, dim3(TriCfg<NP, WV, LPC>::kThreads), TL::kBytes,
                        ctx->stream, Cv, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, npass, e.P1,
                        e.P2, (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips,
                        (int*)ctx->status.ptr, ctx->spin_limit, ctx->report_target, stats);
@@ -2378,18 +2483,32 @@ int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, Ac
 // over more CUs at about half the per-step work (640x480, one frame: strips
 // 0.62 -> 0.41 ms; 4 waves per strip: 0.42 ms, its longer chain of strips
 // eats the shorter steps).  MVSV_OPT_STRIP_WAVES forces either shape.
+template <int NP, int LPC, typename AccT, bool NW>
+int launch_tri_lpc(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
+                   int npass)
+{
+    constexpr int wide = tri_wide_waves<NP, LPC>(), narrow = tri_narrow_waves<NP, LPC>();
+    constexpr int cpw = 64 / LPC;
+    int wv = ctx->strip_waves;
+    if (wv != wide && wv != narrow) {
+        const long long blocks = (long long)npass * n * ((e.W1 + H - 1 + cpw * wide - 1) / (cpw * wide));
+        wv = blocks < ctx->cus ? narrow : wide;
+    }
+    if (wv == narrow) return launch_tri_wv<NP, narrow, LPC, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass);
+    return launch_tri_wv<NP, wide, LPC, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass);
+}
+
+// D = 128 (NP = 4 at 16 lanes per column) may run on 8 lanes per column with
+// 16 disparities per lane (ctx->strip_lpc, MVSV_STRIP_LPC); every other D keeps
+// 16 lanes.  The planes and the cost volume do not depend on the choice.
 template <int NP, typename AccT, bool NW>
 int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
                int npass)
 {
-    constexpr int wide = tri_wide_waves<NP>(), narrow = tri_narrow_waves<NP>();
-    int wv = ctx->strip_waves;
-    if (wv != wide && wv != narrow) {
-        const long long blocks = (long long)npass * n * ((e.W1 + H - 1 + 4 * wide - 1) / (4 * wide));
-        wv = blocks < ctx->cus ? narrow : wide;
+    if constexpr (NP == 4) {
+        if (ctx->strip_lpc == 8) return launch_tri_lpc<8, 8, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass);
     }
-    if (wv == narrow) return launch_tri_wv<NP, narrow, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass);
-    return launch_tri_wv<NP, wide, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass);
+    return launch_tri_lpc<NP, 16, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass);
 }
 
 // Sheared-strip schedule: the down pass ((1,1) (0,1) (-1,1)), the up pass

@@ -2,7 +2,8 @@
 
 Mirrors Stereosystem::initRectification (src/Stereosystem.cpp:193-237: maps from
 cv::initUndistortRectifyMap, CV_32FC1) and Stereosystem::getRectifiedImagepair
-(:243-262: cv::remap INTER_LINEAR on both images, then the mDisplayROI crop).
+(:243-262: cv::remap INTER_LINEAR on both images, then the mDisplayROI crop)
+and its resizing overload (:279-315: cv::resize INTER_LINEAR by a factor).
 The remap runs in a HIP kernel with OpenCV 3.4's fixed-point arithmetic
 (bit-exact for given maps); the map construction is a host double-precision
 restatement (OpenCV inverts P*R by SVD, so a map may differ in the last bit).
@@ -89,3 +90,51 @@ def rectify_pair(left, right, maps, roi):
                                   ctypes.byref(r), oL.ctypes.data, oL.shape[1], oR.ctypes.data,
                                   oR.shape[1]), ctx.handle)
     return oL, oR
+
+
+def resize_size(width, height, fx, fy=None):
+    """Output size of cv::resize(src, dst, Size(0, 0), fx, fy): (cvRound(w fx), cvRound(h fy))."""
+    fy = fx if fy is None else fy
+    w, h = ctypes.c_int(), ctypes.c_int()
+    check(lib().mvsv_resize_size(int(width), int(height), float(fx), float(fy), ctypes.byref(w),
+                                 ctypes.byref(h)))
+    return w.value, h.value
+
+
+def resize(src, fx, fy=None):
+    """cv::resize(src, dst, Size(0, 0), fx, fy, INTER_LINEAR) of a uint8 image
+    (OpenCV 3.4 fixed-point arithmetic, on the GPU).
+
+    src: (H, W) uint8 numpy array (host path), or a (H, W) / (N, H, W) uint8
+    torch tensor on a HIP device (device path, stream-ordered like compute()).
+    """
+    fy = fx if fy is None else fy
+    if type(src).__module__.startswith("torch"):
+        import torch
+        if not (src.is_cuda and src.dtype == torch.uint8 and src.dim() in (2, 3)):
+            raise MvsvError(_lib.MVSV_E_INVALID_ARG, "resize: uint8 device tensor expected")
+        batched = src.dim() == 3
+        s = src if batched else src.unsqueeze(0)
+        if s.stride(2) != 1:
+            s = s.contiguous()
+        n, sh, sw = s.shape
+        dw, dh = resize_size(sw, sh, fx, fy)
+        out = torch.empty((n, dh, dw), dtype=torch.uint8, device=src.device)
+        ctx = context(src.device.index or 0)
+        check(lib().mvsv_set_stream(ctx.handle,
+                                    ctypes.c_void_p(torch.cuda.current_stream(src.device).cuda_stream)),
+              ctx.handle)
+        check(lib().mvsv_resize_device(ctx.handle, n, s.data_ptr(), s.stride(1), s.stride(0), sw, sh,
+                                       float(fx), float(fy), out.data_ptr(), dw, dh * dw), ctx.handle)
+        return out if batched else out[0]
+    a = np.ascontiguousarray(src, np.uint8)
+    if a.ndim != 2:
+        raise MvsvError(_lib.MVSV_E_INVALID_ARG, "resize: a 2-D uint8 image expected")
+    sh, sw = a.shape
+    dw, dh = resize_size(sw, sh, fx, fy)
+    out = np.empty((dh, dw), np.uint8)
+    ctx = context(0)
+    check(lib().mvsv_use_own_stream(ctx.handle), ctx.handle)
+    check(lib().mvsv_resize(ctx.handle, a.ctypes.data, sw, sw, sh, float(fx), float(fy),
+                            out.ctypes.data, dw), ctx.handle)
+    return out

@@ -12,6 +12,7 @@
  */
 #include "mvsv_oracle.h"
 
+#include <float.h>
 #include <limits.h>
 #include <math.h>
 #include <stdlib.h>
@@ -901,4 +902,123 @@ void orc_remap_linear(const uint8_t* src, ptrdiff_t ss, int sw, int sh, const fl
             }
             dst[(size_t)y * dw + x] = (uint8_t)v;
         }
+}
+
+/* [OpenCV 3.4 imgproc/src/resize.cpp] cv::resize(src, dst, Size(0, 0), fx, fy,
+ * INTER_LINEAR) for CV_8UC1 -- the resize of Stereosystem::getRectifiedImagepair
+ * (Stereopair&, float) (src/Stereosystem.cpp:279-315).  TEST INFRASTRUCTURE.
+ *   dsize = (saturate_cast<int>(sw * fx), saturate_cast<int>(sh * fy)) (cvRound);
+ *   scale = 1 / inv_scale; a scale of exactly 2 x 2 runs INTER_AREA's fast path
+ *   (resizeAreaFast_: (a + b + c + d + 2) >> 2 over full 2x2 blocks -- the SIMD
+ *   op and its scalar tail agree -- and a float mean rounded half to even over
+ *   the clipped blocks of an odd edge);
+ *   otherwise resizeGeneric_ with HResizeLinear (exact integer taps, 11-bit
+ *   coefficients saturate_cast<short>(cbuf * 2048), x clamped with fx = 0) and
+ *   VResizeLinear<.., FixedPtCast<int, uchar, 22>>: the CV_SIMD128 op
+ *   (VResizeLinearVec_32s8u) covers x < width - 8 (16- and 8-wide loops) with
+ *   16-bit arithmetic -- s = (S >> 4) per row, mulhi by beta, saturating add,
+ *   (+2) >> 2 -- and the scalar tail x >= width - 8 rounds (sum + 2^21) >> 22.
+ *   Rows clamp to [0, sh - 1] (beta from the unclamped fy). */
+static int orc_round_d(double v) { return (int)lrint(v); }
+
+void orc_resize_linear(const uint8_t* src, ptrdiff_t ss, int sw, int sh, double fx, double fy,
+                       uint8_t* dst, ptrdiff_t ds, int* out_w, int* out_h)
+{
+    const int dw = orc_round_d(sw * fx), dh = orc_round_d(sh * fy);
+    *out_w = dw;
+    *out_h = dh;
+    if (!dst) return;
+    const double scale_x = 1.0 / fx, scale_y = 1.0 / fy;
+    const int isx = orc_round_d(scale_x), isy = orc_round_d(scale_y);
+    const int area_fast = fabs(scale_x - isx) < DBL_EPSILON && fabs(scale_y - isy) < DBL_EPSILON;
+    if (area_fast && isx == 2 && isy == 2) {
+        const int w1 = sw / 2;
+        for (int dy = 0; dy < dh; dy++) {
+            uint8_t* D = dst + (ptrdiff_t)dy * ds;
+            const int sy0 = dy * 2;
+            if (sy0 >= sh) {
+                for (int dx = 0; dx < dw; dx++) D[dx] = 0;
+                continue;
+            }
+            const int w = sy0 + 2 <= sh ? w1 : 0;
+            const uint8_t* S0 = src + (ptrdiff_t)sy0 * ss;
+            int dx = 0;
+            for (; dx < w; dx++) {
+                const int i = 2 * dx;
+                D[dx] = (uint8_t)((S0[i] + S0[i + 1] + S0[ss + i] + S0[ss + i + 1] + 2) >> 2);
+            }
+            for (; dx < dw; dx++) {
+                int sum = 0, count = 0;
+                const int sx0 = 2 * dx;
+                if (sx0 >= sw) {
+                    D[dx] = 0;
+                    continue;
+                }
+                for (int sy = 0; sy < 2 && sy0 + sy < sh; sy++)
+                    for (int sx = 0; sx < 2 && sx0 + sx < sw; sx++) {
+                        sum += src[(ptrdiff_t)(sy0 + sy) * ss + sx0 + sx];
+                        count++;
+                    }
+                int v = (int)lrintf((float)sum / (float)count);
+                D[dx] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+            }
+        }
+        return;
+    }
+    int* xofs = (int*)malloc(sizeof(int) * (size_t)dw);
+    short* ialpha = (short*)malloc(sizeof(short) * 2 * (size_t)dw);
+    int* rows = (int*)malloc(sizeof(int) * 2 * (size_t)dw);
+    for (int dx = 0; dx < dw; dx++) {
+        float f = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)floorf(f);
+        f -= (float)sx;
+        if (sx < 0) f = 0.f, sx = 0;
+        if (sx >= sw - 1) f = 0.f, sx = sw - 1;
+        xofs[dx] = sx;
+        ialpha[2 * dx] = (short)lrintf((1.f - f) * 2048.f);
+        ialpha[2 * dx + 1] = (short)lrintf(f * 2048.f);
+    }
+    for (int dy = 0; dy < dh; dy++) {
+        float f = (float)((dy + 0.5) * scale_y - 0.5);
+        const int sy = (int)floorf(f);
+        f -= (float)sy;
+        const int b0 = (short)lrintf((1.f - f) * 2048.f), b1 = (short)lrintf(f * 2048.f);
+        for (int k = 0; k < 2; k++) {
+            int r = sy + k;
+            r = r < 0 ? 0 : r >= sh ? sh - 1 : r;
+            const uint8_t* S = src + (ptrdiff_t)r * ss;
+            int* o = rows + (size_t)k * dw;
+            for (int dx = 0; dx < dw; dx++) {
+                const int sx = xofs[dx];
+                const int a1 = ialpha[2 * dx + 1];
+                o[dx] = S[sx] * ialpha[2 * dx] + (a1 ? S[sx + 1] * a1 : 0);
+            }
+        }
+        uint8_t* D = dst + (ptrdiff_t)dy * ds;
+        /* columns the SIMD op covers: its 16-wide loop (x <= width - 16), then
+         * its 8-wide loop (x < width - 8) */
+        int simd_end = 0;
+        while (simd_end <= dw - 16) simd_end += 16;
+        while (simd_end < dw - 8) simd_end += 8;
+        for (int x = 0; x < dw; x++) {
+            const int s0 = rows[x], s1 = rows[dw + x];
+            int v;
+            if (x < simd_end) {
+                int h0 = s0 >> 4, h1 = s1 >> 4;
+                h0 = h0 > 32767 ? 32767 : h0 < -32768 ? -32768 : h0;
+                h1 = h1 > 32767 ? 32767 : h1 < -32768 ? -32768 : h1;
+                int r = ((h0 * b0) >> 16) + ((h1 * b1) >> 16);
+                r = r > 32767 ? 32767 : r < -32768 ? -32768 : r;
+                r += 2;
+                r = r > 32767 ? 32767 : r;
+                v = r >> 2;
+            } else {
+                v = (s0 * b0 + s1 * b1 + (1 << 21)) >> 22;
+            }
+            D[x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+        }
+    }
+    free(xofs);
+    free(ialpha);
+    free(rows);
 }

@@ -110,6 +110,12 @@ void orc_reproject(const int16_t* dmap, ptrdiff_t stride, int W, int H, const fl
 void orc_mean_disparity_grid(const int16_t* dmap, ptrdiff_t stride, int W,
                              int H, float* means);
 
+/* cv::resize(src, dst, Size(0, 0), fx, fy, INTER_LINEAR), CV_8UC1 (OpenCV 3.4,
+ * see mvsv_oracle.c): writes the output size to *out_w / *out_h and, when dst
+ * is not NULL, the resized image (row stride ds). */
+void orc_resize_linear(const uint8_t* src, ptrdiff_t ss, int sw, int sh, double fx, double fy,
+                       uint8_t* dst, ptrdiff_t ds, int* out_w, int* out_h);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,6 +64,8 @@ def lib():
         _lib.orc_mean_disparity_grid.argtypes = [P, S, I, I, P]
         _lib.orc_reproject.argtypes = [P, S, I, I, P, P]
         _lib.orc_remap_linear.argtypes = [P, S, I, I, P, P, P, I, I]
+        _lib.orc_resize_linear.argtypes = [P, S, I, I, ctypes.c_double, ctypes.c_double, P, S,
+                                           ctypes.POINTER(I), ctypes.POINTER(I)]
     return _lib
 
 
@@ -173,4 +175,16 @@ def remap_linear(src: np.ndarray, mapx: np.ndarray, mapy: np.ndarray) -> np.ndar
     out = np.empty((dh, dw), np.uint8)
     lib().orc_remap_linear(_ptr(s), s.shape[1], s.shape[1], s.shape[0], _ptr(mx), _ptr(my),
                            _ptr(out), dw, dh)
+    return out
+
+
+def resize_linear(src: np.ndarray, fx: float, fy: float) -> np.ndarray:
+    """cv::resize(src, dst, Size(0, 0), fx, fy, INTER_LINEAR) of a uint8 image."""
+    s = np.ascontiguousarray(src, np.uint8)
+    w, h = ctypes.c_int(), ctypes.c_int()
+    lib().orc_resize_linear(_ptr(s), s.shape[1], s.shape[1], s.shape[0], fx, fy, None, 0,
+                            ctypes.byref(w), ctypes.byref(h))
+    out = np.empty((h.value, w.value), np.uint8)
+    lib().orc_resize_linear(_ptr(s), s.shape[1], s.shape[1], s.shape[0], fx, fy, _ptr(out),
+                            w.value, ctypes.byref(w), ctypes.byref(h))
     return out

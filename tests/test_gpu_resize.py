@@ -1,0 +1,47 @@
+"""cv::resize(INTER_LINEAR) of the resizing getRectifiedImagepair overload
+(src/Stereosystem.cpp:279-315) on the GPU against the oracle's restatement of
+OpenCV 3.4's fixed-point resize (oracle/mvsv_oracle.c orc_resize_linear):
+bit-exact on random images over shrinking / enlarging / 2x2-area factors,
+odd sizes, the host and the device (frame batch) paths."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CASES = [((240, 376), 0.5), ((241, 377), 0.5), ((240, 376), 0.75), ((37, 53), 1.5), ((480, 640), 0.3),
+         ((5, 7), 0.5), ((96, 200), 2.0), ((33, 40), 0.6), ((64, 64), 1.0), ((17, 300), 0.25)]
+
+
+@pytest.mark.parametrize("shape,f", CASES)
+def test_resize_host_matches_oracle(gpu, mvsv, oracle, shape, f):
+    from mvstereovision3_amd import rectify
+    rs = np.random.RandomState(shape[0] * 131 + shape[1])
+    a = rs.randint(0, 256, shape).astype(np.uint8)
+    ff = float(np.float32(f))
+    got = rectify.resize(a, ff, ff)
+    want = oracle.resize_linear(a, ff, ff)
+    assert got.shape == want.shape and np.array_equal(got, want)
+
+
+def test_resize_device_batch_matches_oracle(gpu, mvsv, oracle):
+    import torch
+    from mvstereovision3_amd import rectify
+    rs = np.random.RandomState(7)
+    a = rs.randint(0, 256, (3, 240, 376)).astype(np.uint8)
+    t = torch.from_numpy(a).cuda()
+    for f in (0.5, 0.75, 1.25):
+        got = rectify.resize(t, f).cpu().numpy()
+        for i in range(3):
+            assert np.array_equal(got[i], oracle.resize_linear(a[i], f, f)), (f, i)
+    # an ROI view (row stride > width) on the device
+    v = t[:, 10:200, 20:300]
+    got = rectify.resize(v, 0.5).cpu().numpy()
+    assert np.array_equal(got[1], oracle.resize_linear(a[1, 10:200, 20:300], 0.5, 0.5))
+
+
+def test_resize_rejects_bad_factors(gpu, mvsv):
+    from mvstereovision3_amd import rectify
+    with pytest.raises(mvsv.MvsvError):
+        rectify.resize(np.zeros((10, 10), np.uint8), 0.0)
+    with pytest.raises(mvsv.MvsvError):
+        rectify.resize(np.zeros((10, 10), np.uint8), 0.01)  # empty output

@@ -157,3 +157,32 @@ def test_entry_points_restore_current_device(gpu, mvsv):
     m.compute(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda())
     mvsv.synchronize()
     assert torch.cuda.current_device() == before
+
+
+def test_stream_switch_after_caller_stream_destroyed(gpu, mvsv, oracle):
+    """A device call on a caller-owned HIP stream, the caller destroys that
+    stream, then a host call switches the context to its own stream: the switch
+    waits on the context's own last-use event and never touches the destroyed
+    handle (recording on it was undefined behaviour)."""
+    import ctypes
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so")
+    h = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+    m = sgbm_yml_matcher(mvsv)
+    a = mvsv.synth_pair(SEED0 + 960, 320, 240, 1, 128)
+    b = mvsv.synth_pair(SEED0 + 961, 320, 240, 1, 128)
+    Lt = torch.from_numpy(a[0]).cuda()
+    Rt = torch.from_numpy(a[1]).cuda()
+    ext = torch.cuda.ExternalStream(h.value)
+    with torch.cuda.stream(ext):
+        dev_out = m.compute(Lt, Rt)
+    ext.synchronize()
+    got_a = dev_out.cpu().numpy()
+    del ext
+    assert hip.hipStreamDestroy(h) == 0
+    host_out = m.compute(b[0], b[1])  # switches to the context's own stream
+    p = oracle_params(m)
+    assert np.array_equal(got_a, oracle.sgbm(a[0], a[1], p))
+    assert np.array_equal(host_out, oracle.sgbm(b[0], b[1], p))
+    mvsv.synchronize()

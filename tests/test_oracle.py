@@ -171,3 +171,31 @@ def test_sgbm_saturated_costs_invalid(oracle):
     a = oracle.sgbm(L, R, p, core_only=True)
     assert np.array_equal(a, twin.sgbm_core(L, R, p))
     assert (a == -80).any()
+
+
+def test_oracle_resize_linear_properties(oracle):
+    """orc_resize_linear (cv::resize INTER_LINEAR restatement): factor 1 is the
+    identity, a factor of 0.5 is the rounded 2x2 mean on whole blocks, and every
+    output lies within one grey level of exact bilinear interpolation (OpenCV's
+    pixel-centre convention, x clamped) -- the fixed-point rounding is the only
+    difference.  Parity of the rounding itself is unpinned (OpenCV absent)."""
+    rs = np.random.RandomState(3)
+    a = rs.randint(0, 256, (37, 53)).astype(np.uint8)
+    assert np.array_equal(oracle.resize_linear(a, 1.0, 1.0), a)
+    h = oracle.resize_linear(a, 0.5, 0.5)
+    assert h.shape == (18, 26)  # cvRound(18.5) = 18, cvRound(26.5) = 26 (half to even)
+    q = a[:36, :52].astype(int)
+    blk = (q[0::2, 0::2] + q[1::2, 0::2] + q[0::2, 1::2] + q[1::2, 1::2] + 2) >> 2
+    assert np.array_equal(h, blk)
+    for f in (0.75, 1.5, 0.37, 2.0):
+        r = oracle.resize_linear(a, f, f).astype(float)
+        dh, dw = r.shape
+        xs = np.clip((np.arange(dw) + 0.5) / f - 0.5, 0, 52)
+        ys = np.clip((np.arange(dh) + 0.5) / f - 0.5, 0, 36)
+        x0, y0 = np.floor(xs).astype(int), np.floor(ys).astype(int)
+        x1, y1 = np.minimum(x0 + 1, 52), np.minimum(y0 + 1, 36)
+        ax, ay = xs - x0, (ys - y0)[:, None]
+        A = a.astype(float)
+        ref = (A[y0][:, x0] * (1 - ax) + A[y0][:, x1] * ax) * (1 - ay) + \
+              (A[y1][:, x0] * (1 - ax) + A[y1][:, x1] * ax) * ay
+        assert np.abs(r - ref).max() <= 1.0, f
