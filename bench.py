@@ -15,6 +15,17 @@ median, speckle) with inputs already resident in HBM, plus -- for N > 1 -- the
 RCCL gather of the int16 maps to rank 0 (the only exchange step of the
 frame-parallel batch mode).
 
+Batches in flight (--inflight, default 3): consecutive steps run on separate HIP
+streams, each with its own context (cached volumes) and output, so the kernels of
+one batch overlap those of the next (e.g. the latency-bound final kernel of step
+k beside the cost kernel of step k+1) -- the serving shape of the batch mode;
+every step still computes its whole batch.  value = frames of all K steps / wall
+time.  --inflight 1 runs the steps strictly one after the other
+(single_batch_ms reports that latency in every run).  The roofline's stage
+times come from a separate one-in-flight pass (overlapped launches have no
+kernel duration); profile rocprofv3 runs with --inflight 1 so its kernel
+averages agree.
+
 Run: python bench.py [--gpus N --steps K --warmup W].  With N > 1 and no
 WORLD_SIZE in the environment, bench.py starts the N ranks itself (a child
 `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1`,
@@ -68,6 +79,11 @@ def parse(argv=None):
                     help="CPU baseline threads (0 = the GPU's host-core share, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="batches in flight: consecutive steps on separate HIP streams / contexts "
+                         "(their kernels overlap); 1 = strictly one step after the other")
+    ap.add_argument("--profile-steps", type=int, default=10,
+                    help="steps of the separate one-in-flight pass that times the stages (roofline)")
     ap.add_argument("--force-gather", action="store_true",
                     help="run the multi-rank path even for --gpus 1: torch.distributed.run "
                          "child, NCCL (RCCL) process group, dist.gather of the maps every step")
@@ -270,7 +286,14 @@ def main(argv=None):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     distributed = world > 1 or args.force_gather
+    out_fd = None
     if distributed:
+        # RCCL prints its banner (and any library chatter) on stdout: keep the
+        # process's stdout for the one JSON line and send everything else to
+        # stderr
+        sys.stdout.flush()
+        out_fd = os.dup(1)
+        os.dup2(2, 1)
         dist.init_process_group("nccl", device_id=dev)
 
     W, H, F = args.width, args.height, args.frames
@@ -288,14 +311,27 @@ def main(argv=None):
     # strip schedule when 3 * P2 <= 15 (sgbm.yml: P2 = 5), else u8 / u16
     acc = 0.5 if (D in (32, 64, 128, 256) and 3 * P2 <= 15) else (1 if ndir * P2 <= 255 else 2)
 
-    from mvstereovision3_amd.batch import FrameBatch, frame_seeds
+    from mvstereovision3_amd.batch import FrameBatch, InflightBatches, frame_seeds
     host = [mvsv.synth_pair(sd, W, H, minD, D) for sd in frame_seeds(rank, world, F, SEED0)]
     Lt = torch.from_numpy(np.stack([h[0] for h in host])).to(dev)
     Rt = torch.from_numpy(np.stack([h[1] for h in host])).to(dev)
-    out = torch.empty((F, H, W), dtype=torch.int16, device=dev)
     gather = distributed and not args.no_gather
-    batch = FrameBatch(Lt, Rt, out, lambda L, R, o: m.compute(L, R, o), rank, world, gather,
-                       collective=args.force_gather)
+    compute = lambda L, R, o: m.compute(L, R, o)  # noqa: E731
+    n_in = max(1, args.inflight)
+    if n_in > 1:
+        batch = InflightBatches(Lt, Rt, lambda: torch.empty((F, H, W), dtype=torch.int16, device=dev),
+                                compute, n_in, dev, rank, world, gather, collective=args.force_gather)
+        out = batch.slots[0][2]
+        contexts = batch.contexts()
+    else:
+        out = torch.empty((F, H, W), dtype=torch.int16, device=dev)
+        batch = FrameBatch(Lt, Rt, out, compute, rank, world, gather, collective=args.force_gather)
+        contexts = [_lib.context(local)]
+
+    def check_contexts():
+        # raises if a launch of these steps gave up a strip hand-off (maps INVALID)
+        for c in contexts:
+            _lib.check(_lib.lib().mvsv_synchronize(c.handle), c.handle)
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -303,27 +339,44 @@ def main(argv=None):
             dist.barrier(device_ids=[local])
         torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
+    warm = max(args.warmup, n_in)  # every slot's buffers allocated before timing
+    for _ in range(warm):
         batch.step()
-    ctx = _lib.context(local)
     barrier()
-    _lib.synchronize(local)  # raises if a warm-up launch gave up a strip hand-off
-    _lib.profile_reset(ctx)
-    _lib.profile_enable(ctx, True)
+    check_contexts()
     K = args.steps
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1)]
     t0 = time.perf_counter()
     ev[0].record()
     for i in range(K):
         batch.step()
-        ev[i + 1].record()
+        if n_in == 1:
+            ev[i + 1].record()
     barrier()
     t1 = time.perf_counter()
+    check_contexts()  # no map of the timed steps came from a given-up hand-off
+    elapsed = t1 - t0
+    step_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(K)] if n_in == 1 else None
+    # stage times for the roofline: a separate pass, one step after the other
+    # on the default context (with batches in flight the launches overlap, so
+    # their spans are not kernel durations)
+    ctx = _lib.context(local)
+    pout = torch.empty((F, H, W), dtype=torch.int16, device=dev)
+    compute(Lt, Rt, pout)
+    barrier()
+    _lib.profile_reset(ctx)
+    _lib.profile_enable(ctx, True)
+    P = max(1, args.profile_steps)
+    p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    p0.record()
+    for _ in range(P):
+        compute(Lt, Rt, pout)
+    p1.record()
+    barrier()
     _lib.profile_enable(ctx, False)
     prof = _lib.profile_read(ctx)
-    _lib.synchronize(local)  # no map of the timed steps came from a given-up hand-off
-    elapsed = t1 - t0
-    step_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(K)]
+    _lib.synchronize(local)
+    single_ms = p0.elapsed_time(p1) / P
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -337,7 +390,7 @@ def main(argv=None):
     if rank == 0:
         ms_per_step = elapsed / K * 1e3
         mpix = world * F * W * H * K / elapsed / 1e6
-        stages = {k: {"ms_per_step": v[0] / K, "launches_per_step": v[1] / K}
+        stages = {k: {"ms_per_step": v[0] / P, "launches_per_step": v[1] / P}
                   for k, v in prof.items() if v[1]}
         strips = D in (32, 64, 128, 256)
         # dominant KERNEL: path_aggregation is the span of the strip and line
@@ -377,7 +430,10 @@ def main(argv=None):
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
-            "median_ms_per_step": round(statistics.median(step_ms), 4),
+            "median_ms_per_step": round(statistics.median(step_ms), 4) if step_ms else None,
+            "inflight": n_in,
+            "single_batch_ms": round(single_ms, 4),
+            "single_batch_mpix_s": round(F * W * H / single_ms / 1e3, 2),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -389,6 +445,7 @@ def main(argv=None):
                        "paths": ndir, "frames_per_gpu": F, "global_batch": F * world,
                        "params": "configs/sgbm.yml + mode", "gather": "rccl" if gather else "none",
                        "launch": "torch.distributed.run" if distributed else "single process",
+                       "batches_in_flight": n_in,
                        "parallelism": f"frame-parallel x{world}"},
             "roofline": {"kernel": dom, "bound": bound,
                          "bound_rule": "larger of the measured utilisations hbm_util (PMC traffic) and "
@@ -410,6 +467,7 @@ def main(argv=None):
                                     "achieved_GBps_per_gpu": round(comp * F * K / elapsed / 1e9, 1),
                                     "frac_of_peak": round(comp * F * K / elapsed / 1e9 / HBM_PEAK_GBPS, 5)},
             "stages_ms_per_step": {k: round(v["ms_per_step"], 4) for k, v in stages.items()},
+            "stages_source": f"HIP events around each stage, {P} steps one after the other (no overlap)",
         }
         if world == 1 and not args.no_cpu_baseline:
             info = cpu_info()
@@ -442,7 +500,12 @@ def main(argv=None):
             ok = sum(int(np.array_equal(gathered[r][0], ref[i])) for i, (r, _) in enumerate(sample))
             res["parity_sample_gathered"] = (f"{ok}/{world} gathered frames (frame 0 of each rank, "
                                              f"received on rank 0 through dist.gather) bit-exact vs oracle")
-        print(json.dumps(res), flush=True)
+        line = json.dumps(res)
+        if out_fd is not None:
+            sys.stdout.flush()
+            os.write(out_fd, (line + "\n").encode())
+        else:
+            print(line, flush=True)
     if distributed:
         dist.destroy_process_group()
     return 0

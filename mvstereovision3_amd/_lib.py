@@ -213,7 +213,35 @@ class Context:
 _tls = threading.local()
 
 
+class use_context:
+    """``with use_context(ctx):`` -- this thread's calls on ``ctx.device`` run on
+    ``ctx`` (its own stream-ordered buffers) instead of the thread's default
+    context: independent batches then proceed concurrently on separate
+    contexts / HIP streams (bench.py --inflight)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def __enter__(self):
+        ov = getattr(_tls, "override", None)
+        if ov is None:
+            ov = _tls.override = {}
+        self.prev = ov.get(self.ctx.device)
+        ov[self.ctx.device] = self.ctx
+        return self.ctx
+
+    def __exit__(self, *exc):
+        if self.prev is None:
+            _tls.override.pop(self.ctx.device, None)
+        else:
+            _tls.override[self.ctx.device] = self.prev
+        return False
+
+
 def context(device: int = 0) -> Context:
+    ov = getattr(_tls, "override", None)
+    if ov and device in ov:
+        return ov[device]
     ctxs = getattr(_tls, "ctxs", None)
     if ctxs is None:
         ctxs = _tls.ctxs = {}

@@ -60,3 +60,50 @@ class FrameBatch:
         if self.gather:
             self.gathered = gather_frames(self.out, self.rank, self.world, self.dst, self.collective)
         return self.gathered
+
+
+class InflightBatches:
+    """Consecutive steps of a FrameBatch-style workload with up to ``n`` batches in
+    flight: step k runs on slot k % n -- its own HIP stream, its own mvsv context
+    (cached volumes) and its own output buffer -- so the kernels of consecutive
+    independent batches overlap on the GPU (the serving shape of the
+    frame-parallel batch mode; every step still computes its whole batch).
+    ``compute(L, R, out)`` is called inside the slot's stream and context; the
+    gather (world > 1 or ``collective``) follows it on the same stream, in step
+    order on every rank."""
+
+    def __init__(self, left, right, make_out, compute: Callable, n: int, device, rank: int = 0,
+                 world: int = 1, gather: bool = True, dst: int = 0, collective: bool = False):
+        import torch
+        from ._lib import Context
+        self.left, self.right, self.compute = left, right, compute
+        self.rank, self.world, self.dst, self.collective = rank, world, dst, collective
+        self.gather = gather and (world > 1 or collective)
+        dev = torch.device(device)
+        self.slots = [(torch.cuda.Stream(dev), Context(dev.index or 0), make_out()) for _ in range(n)]
+        self.k = 0
+        self.gathered: Optional[Sequence] = None
+        self.last_out = None
+
+    def step(self):
+        import torch
+        from ._lib import use_context
+        stream, ctx, out = self.slots[self.k % len(self.slots)]
+        self.k += 1
+        stream.wait_stream(torch.cuda.current_stream(stream.device))  # inputs ready
+        with torch.cuda.stream(stream), use_context(ctx):
+            self.compute(self.left, self.right, out)
+            if self.gather:
+                self.gathered = gather_frames(out, self.rank, self.world, self.dst, self.collective)
+        self.last_out = out
+        return self.gathered
+
+    def contexts(self):
+        return [c for _, c, _ in self.slots]
+
+    def join(self):
+        """Make the caller's current stream wait for every slot."""
+        import torch
+        cur = torch.cuda.current_stream(self.slots[0][0].device)
+        for s, _, _ in self.slots:
+            cur.wait_stream(s)

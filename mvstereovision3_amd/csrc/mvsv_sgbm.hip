@@ -1293,6 +1293,9 @@ struct TriCfg {
 #ifndef MVSV_TRI_PF
 #define MVSV_TRI_PF 4
 #endif
+#ifndef MVSV_FINAL_LPR
+#define MVSV_FINAL_LPR 32  // lanes per row of the final kernel for D >= 128 (16: A/B)
+#endif
 #ifndef MVSV_TRI_STEP_SEQ
 #define MVSV_TRI_STEP_SEQ 0  // 1: the three recurrences of a step one after the other (A/B)
 #endif
@@ -2349,7 +2352,7 @@ void launch_final16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const 
     // NP: disparity pairs per lane at 16 lanes per row.  D >= 128: 32 lanes per
     // row (half the pairs per lane, twice the rows in flight per SIMD); a lane
     // keeps >= 2 pairs, so it reads whole 4-disparity nibble groups.
-    constexpr int LPR = NP >= 4 ? 32 : 16;
+    constexpr int LPR = NP >= 4 ? MVSV_FINAL_LPR : 16;
     constexpr int NPL = NP * 16 / LPR;
     constexpr int RPW = 64 / LPR;
     const dim3 grid((H + RPW - 1) / RPW, n);
