@@ -15,7 +15,7 @@ median, speckle) with inputs already resident in HBM, plus -- for N > 1 -- the
 RCCL gather of the int16 maps to rank 0 (the only exchange step of the
 frame-parallel batch mode).
 
-Batches in flight (--inflight, default 3): consecutive steps run on separate HIP
+Batches in flight (--inflight, default 2): consecutive steps run on separate HIP
 streams, each with its own context (cached volumes) and output, so the kernels of
 one batch overlap those of the next (e.g. the latency-bound final kernel of step
 k beside the cost kernel of step k+1) -- the serving shape of the batch mode;
@@ -79,7 +79,7 @@ def parse(argv=None):
                     help="CPU baseline threads (0 = the GPU's host-core share, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=2,
                     help="batches in flight: consecutive steps on separate HIP streams / contexts "
                          "(their kernels overlap); 1 = strictly one step after the other")
     ap.add_argument("--profile-steps", type=int, default=10,

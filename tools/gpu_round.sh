@@ -26,8 +26,8 @@ cd $R
 bash tools/sq_counters.sh $TAG/sq || exit 1
 python tools/sq_summary.py $O/sq $WL $O/sq_summary.json > $O/sq_summary.txt && cp $O/sq_summary.json $P/sq_summary.json || { echo "sq summary failed"; exit 1; }
 cd /tmp
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 2 --warmup 1 > $O/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
-timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 2 --warmup 1 > $O/pmc_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 2 --warmup 1 --inflight 1 --profile-steps 2 > $O/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 2 --warmup 1 --inflight 1 --profile-steps 2 > $O/pmc_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
 cd $R
 python tools/pmc_traffic.py $(find $O/pmc_fetch -name '*counter_collection.csv' | head -1) $(find $O/pmc_write -name '*counter_collection.csv' | head -1) $WL $O/pmc_traffic.json > /dev/null && cp $O/pmc_traffic.json $P/pmc_traffic.json || { echo "pmc summary failed"; exit 1; }
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
@@ -36,5 +36,5 @@ timeout -k 10 600 python bench.py --force-gather --no-cpu-baseline > $O/bench_fo
 timeout -k 10 600 python tools/bench_configs.py > $O/configs.jsonl 2> $O/configs.err || { echo "config table failed"; tail -20 $O/configs.err; exit 1; }
 timeout -k 10 300 python tools/bench_stream.py > $O/stream_config5.json 2> $O/stream.err || { echo "stream bench failed"; exit 1; }
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 10 > $O/trace.log 2>&1 || { echo "trace failed"; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 10 --inflight 1 > $O/trace.log 2>&1 || { echo "trace failed"; exit 1; }
 echo "round ok"
