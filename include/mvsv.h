@@ -247,6 +247,11 @@ MVSV_API int mvsv_stream_set_params(mvsv_stream* s, const mvsv_sgbm_params* p);
  * kernels for up to batch-1 frames of extra latency; pop / set_params launch a
  * partial group when they need its frames */
 MVSV_API int mvsv_stream_set_batch(mvsv_stream* s, int batch);
+/* up to n (1..4, default 1) frame-batch launches in flight at once: launches go
+ * round-robin to the caller's context and n-1 contexts the stream creates on the
+ * same device (own HIP stream and scratch each; kernel options copied from the
+ * caller's context) -- one launch's latency-bound kernels overlap the next's */
+MVSV_API int mvsv_stream_set_inflight(mvsv_stream* s, int n);
 /* MVSV_E_INVALID_ARG when depth frames are already pending (pop first) */
 MVSV_API int mvsv_stream_push(mvsv_stream* s, const uint8_t* left, size_t left_stride,
                               const uint8_t* right, size_t right_stride);

@@ -274,6 +274,8 @@ public:
     void setParams(const StereoSGBM& matcher) { check(mvsv_stream_set_params(s_, &matcher.params()), ctx_); }
     // frames computed `batch` at a time (frame-batch kernels, up to batch-1 frames of latency)
     void setBatch(int batch) { check(mvsv_stream_set_batch(s_, batch), ctx_); }
+    // up to n frame-batch launches computed concurrently (1..4)
+    void setInflight(int n) { check(mvsv_stream_set_inflight(s_, n), ctx_); }
     int pending() const { return mvsv_stream_pending(s_); }
     void push(const Stereopair& s)
     {

@@ -133,6 +133,7 @@ def _declare(lib, strict=True):
         "mvsv_stream_create": ([P, I, I, P, I, P, ctypes.POINTER(P)], I),
         "mvsv_stream_set_params": ([P, P], I),
         "mvsv_stream_set_batch": ([P, I], I),
+        "mvsv_stream_set_inflight": ([P, I], I),
         "mvsv_stream_push": ([P, P, Z, P, Z], I),
         "mvsv_stream_pop": ([P, P, Z, P], I),
         "mvsv_stream_pending": ([P], I),

@@ -13,6 +13,11 @@
 // consecutive slots is one frame-batch launch (sustained rate of the batch
 // kernels instead of the single-frame ones, at b frames of extra latency);
 // pop and set_params launch a partial group when they need to.
+// With mvsv_stream_set_inflight(n), consecutive launches go round-robin to n
+// compute lanes: the caller's context and n-1 contexts the stream owns (each
+// its own HIP stream and scratch buffers), so up to n frame-batch launches run
+// concurrently and one fills the chip's gaps left by another's
+// latency-bound kernels.
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -22,8 +27,12 @@
 
 using namespace mvsv;
 
+static constexpr int kStreamMaxInflight = 4;
+
 struct mvsv_stream {
     mvsv_ctx* ctx = nullptr;
+    std::vector<mvsv_ctx*> lanes;  // [0] = ctx; the rest are owned by the stream
+    long runs = 0;                 // launches enqueued (lane = runs % lanes)
     int W = 0, H = 0;
     mvsv_sgbm_params params{};
     SgbmEff eff{};
@@ -57,6 +66,7 @@ struct mvsv_stream {
 
 static void stream_free(mvsv_stream* st)
 {
+    for (size_t i = 1; i < st->lanes.size(); i++) mvsv_destroy(st->lanes[i]);
     for (auto& s : st->slots) {
         if (s.hL) (void)hipHostFree(s.hL);
         if (s.hR) (void)hipHostFree(s.hR);
@@ -92,6 +102,7 @@ int mvsv_stream_create(mvsv_ctx* ctx, int W, int H, const mvsv_sgbm_params* p, i
     mvsv_stream* st = new (std::nothrow) mvsv_stream();
     if (!st) return MVSV_E_OOM;
     st->ctx = ctx;
+    st->lanes.push_back(ctx);
     st->W = W;
     st->H = H;
     st->params = *p;
@@ -135,7 +146,6 @@ int mvsv_stream_create(mvsv_ctx* ctx, int W, int H, const mvsv_sgbm_params* p, i
 // frame-batch launch per run of consecutive slots (a run ends at the ring's end).
 static int stream_launch(mvsv_stream* st)
 {
-    mvsv_ctx* ctx = st->ctx;
     const int W = st->W, H = st->H;
     const size_t px = (size_t)W * H;
     const long depth = (long)st->slots.size();
@@ -146,6 +156,7 @@ static int stream_launch(mvsv_stream* st)
         const int n = run.n;
         auto& first = st->slots[i0];
         auto& last = st->slots[i0 + n - 1];
+        mvsv_ctx* ctx = st->lanes[st->runs % (long)st->lanes.size()];
         // the upload stream is in order: the last slot's upload covers the run
         if ((rc = check_hip(ctx, hipStreamWaitEvent(ctx->stream, last.uploaded, 0), "stream wait")))
             return rc;
@@ -161,21 +172,26 @@ static int stream_launch(mvsv_stream* st)
             status = mean_grid_device(ctx, n, first.dOut + (size_t)q.y0 * W + q.x0, W, px, q.x1 - q.x0,
                                       q.y1 - q.y0, first.dMeans);
         }
+        if (status != MVSV_OK && ctx != st->ctx) st->ctx->err = ctx->err;  // reported by pop
+        st->runs++;
         if ((rc = mark_last_use(ctx, MVSV_OK)) ||
             (rc = check_hip(ctx, hipEventRecord(last.computed, ctx->stream), "stream event")) ||
-            (rc = check_hip(ctx, hipStreamWaitEvent(st->down, last.computed, 0), "stream wait")))
+            (rc = check_hip(ctx, hipStreamWaitEvent(st->down, last.computed, 0), "stream wait"))) {
+            if (ctx != st->ctx) st->ctx->err = ctx->err;
             return rc;
+        }
         for (int k = 0; k < n; k++) {
             auto& s = st->slots[i0 + k];
             s.status = status;
-            if ((rc = check_hip(ctx, hipMemcpyAsync(s.hOut, s.dOut, px * 2, hipMemcpyDeviceToHost, st->down),
+            mvsv_ctx* c = st->ctx;
+            if ((rc = check_hip(c, hipMemcpyAsync(s.hOut, s.dOut, px * 2, hipMemcpyDeviceToHost, st->down),
                                 "stream D2H")))
                 return rc;
             if (st->grid &&
-                (rc = check_hip(ctx, hipMemcpyAsync(s.hMeans, s.dMeans, 81 * sizeof(float),
-                                                    hipMemcpyDeviceToHost, st->down), "stream D2H")))
+                (rc = check_hip(c, hipMemcpyAsync(s.hMeans, s.dMeans, 81 * sizeof(float),
+                                                  hipMemcpyDeviceToHost, st->down), "stream D2H")))
                 return rc;
-            if ((rc = check_hip(ctx, hipEventRecord(s.done, st->down), "stream event"))) return rc;
+            if ((rc = check_hip(c, hipEventRecord(s.done, st->down), "stream event"))) return rc;
         }
         st->launched += n;
     }
@@ -191,6 +207,45 @@ int mvsv_stream_set_batch(mvsv_stream* st, int batch)
     int rc = stream_launch(st);  // frames already pushed keep the old grouping
     if (rc) return rc;
     st->batch = batch;
+    return MVSV_OK;
+}
+
+// The stream's own lanes follow the caller context's kernel options.
+static void copy_options(mvsv_ctx* d, const mvsv_ctx* s)
+{
+    d->spin_limit = s->spin_limit;
+    d->path16 = s->path16;
+    d->cost2 = s->cost2;
+    d->cost_ty = s->cost_ty;
+    d->tri = s->tri;
+    d->path_sched = s->path_sched;
+    d->strip_waves = s->strip_waves;
+    d->strip_lpc = s->strip_lpc;
+    d->lines_aux = s->lines_aux;
+    d->bm2 = s->bm2;
+    d->bm_ty = s->bm_ty;
+}
+
+int mvsv_stream_set_inflight(mvsv_stream* st, int n)
+{
+    if (!st) return MVSV_E_INVALID_ARG;
+    mvsv_ctx* ctx = st->ctx;
+    if (n < 1 || n > kStreamMaxInflight)
+        return set_error(ctx, MVSV_E_INVALID_ARG, "stream launches in flight must be 1..4");
+    DeviceGuard dev_guard(ctx->device);
+    int rc = stream_launch(st);  // frames already pushed keep the old lanes
+    if (rc) return rc;
+    while ((int)st->lanes.size() < n) {
+        mvsv_ctx* c = nullptr;
+        if ((rc = mvsv_create(&c, ctx->device))) return set_error(ctx, rc, "stream lane context creation failed");
+        copy_options(c, ctx);
+        st->lanes.push_back(c);
+    }
+    while ((int)st->lanes.size() > n) {  // mvsv_destroy waits for the lane's work
+        mvsv_destroy(st->lanes.back());
+        st->lanes.pop_back();
+    }
+    st->runs = 0;
     return MVSV_OK;
 }
 
@@ -281,7 +336,7 @@ void mvsv_stream_destroy(mvsv_stream* st)
     if (!st) return;
     DeviceGuard dev_guard(st->ctx->device);
     (void)hipStreamSynchronize(st->up);
-    (void)hipStreamSynchronize(st->ctx->stream);
+    for (mvsv_ctx* c : st->lanes) (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(st->down);
     stream_free(st);
 }

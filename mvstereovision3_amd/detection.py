@@ -198,10 +198,12 @@ class DisparityStream:
     push(left, right) uploads a rectified pair and enqueues SGBM (+ the 9x9
     mean grid of grid_roi); pop() returns (disparity int16, means[81] or None)
     in push order.  `depth` frames may be in flight; with batch > 1 they are
-    computed in groups of `batch` frames (frame-batch kernels).
+    computed in groups of `batch` frames (frame-batch kernels); with inflight > 1
+    up to that many groups run concurrently on the stream's compute lanes.
     """
 
-    def __init__(self, matcher, width, height, depth=3, grid_roi=None, device=0, batch=1):
+    def __init__(self, matcher, width, height, depth=3, grid_roi=None, device=0, batch=1,
+                 inflight=1):
         self._ctx = context(device)
         self.width, self.height = width, height
         self._params = matcher._params
@@ -214,6 +216,12 @@ class DisparityStream:
         self._h = h
         if batch != 1:
             self.set_batch(batch)
+        if inflight != 1:
+            self.set_inflight(inflight)
+
+    def set_inflight(self, n):
+        """Up to n frame-batch launches in flight (mvsv_stream_set_inflight)."""
+        check(lib().mvsv_stream_set_inflight(self._h, int(n)), self._ctx.handle)
 
     def set_batch(self, batch):
         """Compute frames `batch` at a time (mvsv_stream_set_batch)."""

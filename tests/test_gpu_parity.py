@@ -449,14 +449,16 @@ def test_disparity_stream_matches_direct_compute(gpu, mvsv, oracle):
         assert np.array_equal(means, oracle.mean_disparity_grid(np.ascontiguousarray(want[y0:y1, x0:x1])))
 
 
-@pytest.mark.parametrize("depth,batch", [(4, 2), (5, 3), (6, 6)])
-def test_disparity_stream_batched(gpu, mvsv, oracle, depth, batch):
-    """Frames computed `batch` at a time: partial groups on pop, a parameter change
-    mid-group, groups cut at the slot ring's end -- every frame still matches."""
+@pytest.mark.parametrize("depth,batch,inflight", [(4, 2, 1), (5, 3, 1), (6, 6, 1), (6, 2, 2),
+                                                  (7, 2, 3), (5, 1, 4)])
+def test_disparity_stream_batched(gpu, mvsv, oracle, depth, batch, inflight):
+    """Frames computed `batch` at a time, `inflight` launches at once on the stream's
+    compute lanes: partial groups on pop, a parameter change mid-group, groups cut
+    at the slot ring's end -- every frame still matches."""
     W, H, D = 256, 64, 64
     m = mvsv.StereoSGBM.create(0, D, 7, 8 * 49, 32 * 49)
     roi_u, _ = mvsv.create_dmap_rois((H, W), D)
-    st = mvsv.DisparityStream(m, W, H, depth=depth, grid_roi=roi_u, batch=batch)
+    st = mvsv.DisparityStream(m, W, H, depth=depth, grid_roi=roi_u, batch=batch, inflight=inflight)
     frames = [mvsv.synth_pair(SEED0 + 60 + i, W, H, 0, D) for i in range(11)]
     got, uq_from = [], 7
     for i, (L, R) in enumerate(frames):
@@ -465,6 +467,8 @@ def test_disparity_stream_batched(gpu, mvsv, oracle, depth, batch):
         if i == uq_from:
             m.setUniquenessRatio(10)
             st.set_params(m)
+        if i == 9 and inflight > 1:
+            st.set_inflight(inflight - 1)  # lanes dropped with launches in flight
         st.push(L, R)
     while st.pending():
         got.append(st.pop())

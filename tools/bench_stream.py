@@ -9,7 +9,7 @@ Host frames go in, int16 maps and the 81 tile means come back (PCIe included);
 `depth` frames are in flight, computed `batch` at a time.  Also reports the device-resident rate of the same
 matcher on a batch of 8 frames.  Not the headline metric (bench.py is).
 
-    python tools/bench_stream.py [--frames 300] [--depth 16] [--batch 8]
+    python tools/bench_stream.py [--frames 300] [--depth 24] [--batch 8] [--inflight 2]
 """
 import argparse
 import json
@@ -24,8 +24,10 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=300)
-    ap.add_argument("--depth", type=int, default=16)
+    ap.add_argument("--depth", type=int, default=24)
     ap.add_argument("--batch", type=int, default=8, help="frames per SGBM launch (mvsv_stream_set_batch)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="launches computed concurrently (mvsv_stream_set_inflight)")
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=960)
     a = ap.parse_args()
@@ -45,25 +47,34 @@ def main():
     det.init((roi_u[3] - roi_u[1], roi_u[2] - roi_u[0]), Q, 0.1, 1.5)
     uniq = [mvsv.synth_pair(0x5EED0000 + i, W, H, 0, D) for i in range(8)]
 
-    st = mvsv.DisparityStream(m, W, H, depth=a.depth, grid_roi=roi_u, batch=a.batch)
+    st = mvsv.DisparityStream(m, W, H, depth=a.depth, grid_roi=roi_u, batch=a.batch,
+                              inflight=a.inflight)
     found = 0
+    host = {"push": 0.0, "pop": 0.0, "post": 0.0}
 
     def consume():
         nonlocal found
+        t = time.perf_counter()
         d, means = st.pop()
+        t2 = time.perf_counter()
         det.build(d, 0, det.MEAN_VALUE, means=means)
         det.detectObstacles(write_pcl=False)
         found += len(det.getFoundObstacles())
+        host["pop"] += t2 - t
+        host["post"] += time.perf_counter() - t2
 
     for i in range(a.depth):  # warm-up
         st.push(*uniq[i % 8])
     while st.pending():
         consume()
+    host = dict.fromkeys(host, 0.0)
     t0 = time.perf_counter()
     for i in range(a.frames):
         if st.pending() == a.depth:
             consume()
+        t = time.perf_counter()
         st.push(*uniq[i % 8])
+        host["push"] += time.perf_counter() - t
     while st.pending():
         consume()
     wall = time.perf_counter() - t0
@@ -86,13 +97,14 @@ def main():
     dwall = time.perf_counter() - t1
     print(json.dumps({
         "workload": f"config5_stream_{W}x{H}_d{D}_mode_sgbm",
-        "frames": a.frames, "depth": a.depth, "batch": a.batch,
+        "frames": a.frames, "depth": a.depth, "batch": a.batch, "inflight": a.inflight,
         "stream_fps": round(a.frames / wall, 2),
         "stream_mpix_s": round(a.frames * W * H / wall / 1e6, 2),
         "stream_ms_per_frame": round(wall / a.frames * 1e3, 3),
         "device_resident_mpix_s": round(8 * steps * W * H / dwall / 1e6, 2),
         "device_resident_ms_per_frame": round(dwall / (8 * steps) * 1e3, 3),
         "obstacle_tiles_found": found,
+        "host_ms_per_frame": {k: round(v / a.frames * 1e3, 3) for k, v in host.items()},
         "note": "stream = host frames in, int16 map + 81 means out (PCIe incl.); "
                 "post-pass = MeanDisparityDetection build(MEAN_VALUE) + detectObstacles",
     }))

@@ -1,4 +1,4 @@
-"""Timings of the StereoBM match kernels (tools/bm_quick.sh): configs 1 / 2 at
+"""Timings of the StereoBM match kernels (run on the box: python tools/bm_time.py): configs 1 / 2 at
 batch 1 and 8, the disparities-on-lanes kernel with the chosen tile height and
 a sweep of MVSV_BM_TY, then the 16x16-tile kernel (MVSV_KERNELS=bm-tile)."""
 import os

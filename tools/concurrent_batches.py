@@ -21,16 +21,21 @@ def main():
     ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--mode", type=int, default=1)
+    ap.add_argument("--config5", action="store_true",
+                    help="liveDisparity parameters: create(0, 256, 9, 648, 2592), MODE_SGBM")
     a = ap.parse_args()
     import numpy as np
     import torch
     import mvstereovision3_amd as mvsv
     from mvstereovision3_amd import _lib
     W, H, F = 1280, 960, a.frames
-    m = mvsv.StereoSGBM.create(0, 0, 0, 0, 0)
-    mvsv.Disparity.loadSGBMParameters(os.path.join(ROOT, "tests/golden/configs/sgbm.yml"), m,
-                                      mvsv.sgbmParameters())
-    m.setMode(a.mode)
+    if a.config5:
+        m = mvsv.StereoSGBM.create(0, 256, 9, 648, 2592)
+    else:
+        m = mvsv.StereoSGBM.create(0, 0, 0, 0, 0)
+        mvsv.Disparity.loadSGBMParameters(os.path.join(ROOT, "tests/golden/configs/sgbm.yml"), m,
+                                          mvsv.sgbmParameters())
+        m.setMode(a.mode)
     pd = m.params()
     host = [mvsv.synth_pair(0x5EED0000 + i, W, H, pd["min_disparity"], pd["num_disparities"])
             for i in range(F)]
