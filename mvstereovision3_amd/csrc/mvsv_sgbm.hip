@@ -1375,7 +1375,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
     const int16_t* __restrict__ C, AccT* __restrict__ A, size_t plane, AccT* __restrict__ dummy,
     int H, int W1, int D, int npass, int P1, int P2, unsigned long long* __restrict__ bnd,
     unsigned epoch, int nframes, int nstrips, int* __restrict__ status, unsigned spin_limit,
-    int* __restrict__ report, unsigned long long* __restrict__ stats)
+    int* __restrict__ report, unsigned long long* __restrict__ stats, int trace_h)
 {
     using AV = AccVec<NP, AccT>;
     using TL = TriLayout<NP, WV, LPC>;
@@ -1429,7 +1429,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
     auto mcol = [&](int buf, int dir, int c) -> int* { return lmin + (buf * 2 + dir) * TL::kCols + c; };
 
     // zero both LDS rows (cells outside the image / before the first step)
-    for (int i = threadIdx.x; i < TL::kLDw + TL::kMinInts; i += 64 * (kTriWaves + 1)) lds[i] = 0u;
+    for (int i = threadIdx.x; i < TL::kLDw + TL::kMinInts; i += TriCfg<NP, WV, LPC>::kThreads) lds[i] = 0u;
 
     // ---- comm wave: lanes (item j = min(r, 2), rl); row 3 repeats item 2's
     // loads and stores at item 2's own addresses (same values: the duplicate
@@ -1517,6 +1517,8 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
         unsigned long long* q = pdst + (size_t)clampi(t, 0, H - 1) * bstep;
 #pragma unroll
         for (int i = 0; i < NG; i++) __hip_atomic_store(q + 4 * LPC * i, g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (trace_h && lane == 0)  // MVSV_TRI_TRACE: when step t went out (100 MHz clock)
+            stats[(size_t)blockIdx.x * (8 + 2 * trace_h) + 8 + t] = __builtin_amdgcn_s_memrealtime();
     };
 
     // ---- compute waves ----
@@ -1558,6 +1560,8 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
         const int cur = i & 1, prv = cur ^ 1;
         if (i > 0) publish(t - 1, prv);
         bconsume(t, cur, bg[j % BF]);
+        if (trace_h && lane == 0)  // when the producer's step t was in
+            stats[(size_t)blockIdx.x * (8 + 2 * trace_h) + 8 + trace_h + t] = __builtin_amdgcn_s_memrealtime();
         bload(t + BF, bg[j % BF]);
         __syncthreads();
     };
@@ -1701,7 +1705,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
     if (comm) {
         publish(te - 1, (len - 1) & 1);
         if (stats && lane == 0) {
-            unsigned long long* q = stats + (size_t)blockIdx.x * 8;
+            unsigned long long* q = stats + (size_t)blockIdx.x * (8 + 2 * trace_h);
             q[0] = st_t0;
             q[1] = __builtin_amdgcn_s_memtime();
             q[2] = st_spin;
@@ -2434,10 +2438,15 @@ int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, Ac
     const unsigned epoch = ctx->tri_epoch;
     dim3 grid(nstrips * npass * n);
     unsigned long long* stats = nullptr;
-    const bool want_stats = std::getenv("MVSV_TRI_STATS") != nullptr;
+    // MVSV_TRI_STATS: per-strip summary on stderr; MVSV_TRI_TRACE=path: also
+    // every step's publish / consume time (100 MHz) of every strip, to a file
+    const char* trace_path = std::getenv("MVSV_TRI_TRACE");
+    const bool want_stats = std::getenv("MVSV_TRI_STATS") != nullptr || trace_path;
+    const int trace_h = trace_path ? H : 0;
+    const size_t sb = 8 + 2 * (size_t)trace_h;  // u64 per block
     if (want_stats) {
-        (void)hipMalloc(&stats, (size_t)grid.x * 64);
-        (void)hipMemset(stats, 0, (size_t)grid.x * 64);
+        (void)hipMalloc(&stats, (size_t)grid.x * sb * 8);
+        (void)hipMemset(stats, 0, (size_t)grid.x * sb * 8);
     }
     if (TL::kBytes > 65536 &&
         (rc = check_hip(ctx, hipFuncSetAttribute((const void*)sgbm_tri_kernel<NP, WV, LPC, AccT, NW>,
@@ -2447,16 +2456,26 @@ int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, Ac
     hipLaunchKernelGGL((sgbm_tri_kernel<NP, WV, LPC, AccT, NW>), grid, dim3(TriCfg<NP, WV, LPC>::kThreads), TL::kBytes,
                        ctx->stream, Cv, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, npass, e.P1,
                        e.P2, (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips,
-                       (int*)ctx->status.ptr, ctx->spin_limit, ctx->report_target, stats);
+                       (int*)ctx->status.ptr, ctx->spin_limit, ctx->report_target, stats, trace_h);
     rc = check_hip(ctx, hipGetLastError(), "sgbm sheared-strip path kernel");
     if (want_stats) {
         (void)hipStreamSynchronize(ctx->stream);
-        std::vector<unsigned long long> h((size_t)grid.x * 8);
+        std::vector<unsigned long long> h((size_t)grid.x * sb);
         (void)hipMemcpy(h.data(), stats, h.size() * 8, hipMemcpyDeviceToHost);
         (void)hipFree(stats);
+        if (trace_path) {
+            if (FILE* fp = std::fopen(trace_path, "wb")) {
+                const unsigned long long hdr[8] = {grid.x, sb, (unsigned long long)H, (unsigned long long)nstrips,
+                                                   (unsigned long long)npass, (unsigned long long)n,
+                                                   (unsigned long long)kTriSW, (unsigned long long)e.W1};
+                std::fwrite(hdr, 8, 8, fp);
+                std::fwrite(h.data(), 8, h.size(), fp);
+                std::fclose(fp);
+            }
+        }
         unsigned long long t0 = ~0ull, t1 = 0, spin = 0, busy = 0, steps = 0, longest = 0, lst = 0;
         for (size_t b = 0; b < grid.x; b++) {
-            const unsigned long long* q = &h[b * 8];
+            const unsigned long long* q = &h[b * sb];
             if (!q[1]) continue;
             t0 = std::min(t0, q[0]);
             t1 = std::max(t1, q[1]);
@@ -2470,7 +2489,7 @@ int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, Ac
                      t1 - t0, grid.x, busy, spin, 100.0 * spin / std::max(busy, 1ull),
                      (double)busy / std::max(steps, 1ull), longest, lst);
         for (size_t b = 0; b < grid.x; b += grid.x / 24 + 1) {
-            const unsigned long long* q = &h[b * 8];
+            const unsigned long long* q = &h[b * sb];
             std::fprintf(stderr, "[tri]  blk %zu k %llu pass %llu tb %llu len %llu start %llu dur %llu spin %llu n %llu\n",
                          b, q[5], q[6], q[7], q[4], q[0] - t0, q[1] - q[0], q[2], q[3]);
         }

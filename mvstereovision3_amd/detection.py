@@ -247,10 +247,11 @@ class DisparityStream:
         check(lib().mvsv_stream_push(self._h, L.ctypes.data, L.strides[0], R.ctypes.data,
                                      R.strides[0]), self._ctx.handle)
 
-    def pop(self):
-        out = np.empty((self.height, self.width), np.int16)
+    def pop(self, copy_map=True):
+        """(map, means) of the oldest frame; copy_map=False returns (None, means)."""
+        out = np.empty((self.height, self.width), np.int16) if copy_map else None
         means = np.empty(81, np.float32) if self._grid else None
-        check(lib().mvsv_stream_pop(self._h, out.ctypes.data, self.width,
+        check(lib().mvsv_stream_pop(self._h, out.ctypes.data if out is not None else None, self.width,
                                     means.ctypes.data if means is not None else None),
               self._ctx.handle)
         return out, means

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--batch", type=int, default=8, help="frames per SGBM launch (mvsv_stream_set_batch)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="launches computed concurrently (mvsv_stream_set_inflight)")
+    ap.add_argument("--host-probe", choices=["full", "no-post", "no-copy"], default="full",
+                    help="diagnostics: skip the detection post-pass, or also the map copy of pop")
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=960)
     a = ap.parse_args()
@@ -55,11 +57,15 @@ def main():
     def consume():
         nonlocal found
         t = time.perf_counter()
-        d, means = st.pop()
+        if a.host_probe == "no-copy":
+            st.pop(copy_map=False)
+        else:
+            d, means = st.pop()
         t2 = time.perf_counter()
-        det.build(d, 0, det.MEAN_VALUE, means=means)
-        det.detectObstacles(write_pcl=False)
-        found += len(det.getFoundObstacles())
+        if a.host_probe == "full":
+            det.build(d, 0, det.MEAN_VALUE, means=means)
+            det.detectObstacles(write_pcl=False)
+            found += len(det.getFoundObstacles())
         host["pop"] += t2 - t
         host["post"] += time.perf_counter() - t2
 
@@ -98,6 +104,7 @@ def main():
     print(json.dumps({
         "workload": f"config5_stream_{W}x{H}_d{D}_mode_sgbm",
         "frames": a.frames, "depth": a.depth, "batch": a.batch, "inflight": a.inflight,
+        "host_probe": a.host_probe,
         "stream_fps": round(a.frames / wall, 2),
         "stream_mpix_s": round(a.frames * W * H / wall / 1e6, 2),
         "stream_ms_per_frame": round(wall / a.frames * 1e3, 3),
