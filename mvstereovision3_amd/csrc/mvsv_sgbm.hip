@@ -1293,6 +1293,9 @@ struct TriCfg {
 #ifndef MVSV_TRI_PF
 #define MVSV_TRI_PF 4
 #endif
+#ifndef MVSV_FINAL32_PF
+#define MVSV_FINAL32_PF 8  // steps of prefetch in the 32-lanes-per-row final kernel
+#endif
 #ifndef MVSV_FINAL_LPR
 #define MVSV_FINAL_LPR 32  // lanes per row of the final kernel for D >= 128 (16: A/B)
 #endif
@@ -1953,7 +1956,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     constexpr int NW = AR::NW;
     // 32 lanes per row: twice the waves, so a shallower prefetch keeps the
     // kernel at <= 128 VGPRs (4 waves per SIMD)
-    constexpr int PF = LPR == 32 ? 8 : final16_pf<NP, NACC, AccT, UQ>();
+    constexpr int PF = LPR == 32 ? MVSV_FINAL32_PF : final16_pf<NP, NACC, AccT, UQ>();
     constexpr int RPW = 64 / LPR;     // image rows per wave
     constexpr int DR = 2 * NP * LPR;  // disparities of a row (D)
     // S of the current step, one D-vector per row: S[best -+ 1] come back
@@ -2069,6 +2072,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
             for (int p = 0; p < NP; p++) o.v[p] = st[p];
             o.store((int16_t*)(ms + d0));
         }
+        // the wave barriers order the lanes' LDS hand-over for the compiler
+        // (without them it moved accesses across lanes' writes: wrong maps)
         __builtin_amdgcn_wave_barrier();
         const int bm = max(best - 1, 0), bp = min(best + 1, DR - 1);
         const int Sm = ms[bm], Sp = ms[bp];
