@@ -105,7 +105,12 @@ enum {
      * at most half the GPU with sheared strips (one camera frame; needs
      * P2 <= 15),
      * sheared strips otherwise; 1 = strips; 2 = directions side by side */
-    MVSV_OPT_PATH_SCHEDULE = 4
+    MVSV_OPT_PATH_SCHEDULE = 4,
+    /* which strip a block of the sheared-strip kernel runs: 1 (default) = a
+     * ticket drawn on arrival, so a strip only waits on a strip already
+     * running or done whatever the dispatch order; 0 = its blockIdx (relies
+     * on in-order dispatch; keeps a strip chain on one XCD, a few % faster) */
+    MVSV_OPT_STRIP_TICKETS = 5
 };
 
 /* StereoSGBM modes (cv::StereoSGBM::MODE_SGBM / MODE_HH). */

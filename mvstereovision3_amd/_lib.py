@@ -29,6 +29,7 @@ OPT_STRIP_SPIN_LIMIT = 1
 OPT_BM_TILE_ROWS = 2
 OPT_STRIP_WAVES = 3
 OPT_PATH_SCHEDULE = 4
+OPT_STRIP_TICKETS = 5
 
 MODE_SGBM = 0
 MODE_HH = 1

@@ -282,6 +282,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
         (void)hipGetLastError();
         c->cus = 256;
     }
+    if (const char* v = std::getenv("MVSV_STRIP_ORDER")) c->strip_tickets = std::strcmp(v, "blockidx") != 0;
     if (const char* v = std::getenv("MVSV_LINES_AUX")) c->lines_aux = std::max(-1, std::min(2, std::atoi(v)));
     *out = c;
     return MVSV_OK;
@@ -425,6 +426,10 @@ int mvsv_set_option(mvsv_ctx* ctx, int option, long long value)
     case MVSV_OPT_STRIP_WAVES:
         if (value < 0 || value > 64) return set_error(ctx, MVSV_E_INVALID_ARG, "strip waves must be 0..64");
         ctx->strip_waves = (int)value;
+        return MVSV_OK;
+    case MVSV_OPT_STRIP_TICKETS:
+        if (value < 0 || value > 1) return set_error(ctx, MVSV_E_INVALID_ARG, "strip tickets must be 0 or 1");
+        ctx->strip_tickets = (int)value;
         return MVSV_OK;
     default:
         return set_error(ctx, MVSV_E_INVALID_ARG, "unknown option");

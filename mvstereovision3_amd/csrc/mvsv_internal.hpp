@@ -94,6 +94,11 @@ struct mvsv_ctx {
     // boundary granules (tri_bnd is re-zeroed whenever they wrap), all 32 bits
     // go into status[0] when that launch gives up a wait (no per-call reset)
     unsigned tri_epoch = 0;
+    // strip blocks draw their strip as a ticket (status[2]) unless strip_tickets
+    // is 0 (blockIdx order, MVSV_STRIP_ORDER=blockidx); tri_tickets = the first
+    // ticket of the next launch (the counter is zeroed with the status word)
+    int strip_tickets = 1;
+    unsigned tri_tickets = 0;
     unsigned spin_limit = mvsv::kStripSpinLimitDefault;
     // given-up strip waits are reported into host-mapped ints: `report` is the
     // context's sticky word (device calls; read and cleared by the next call,

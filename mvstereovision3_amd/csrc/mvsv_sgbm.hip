@@ -1378,7 +1378,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
     const int16_t* __restrict__ C, AccT* __restrict__ A, size_t plane, AccT* __restrict__ dummy,
     int H, int W1, int D, int npass, int P1, int P2, unsigned long long* __restrict__ bnd,
     unsigned epoch, int nframes, int nstrips, int* __restrict__ status, unsigned spin_limit,
-    int* __restrict__ report, unsigned long long* __restrict__ stats, int trace_h)
+    int* __restrict__ report, unsigned long long* __restrict__ stats, int trace_h, long long ticket0)
 {
     using AV = AccVec<NP, AccT>;
     using TL = TriLayout<NP, WV, LPC>;
@@ -1396,13 +1396,33 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool comm = w == kTriWaves;
     const int r = lane / LPC, rl = lane % LPC;
-    // strips counted from the right; passes and frames interleaved, so every
-    // block's producer (same pass and frame, strip k-1) has a lower index.
-    // Pass 0 sweeps down (sy = +1), pass 1 up (sy = -1), each into its own
-    // accumulator plane.
+    // strips counted from the right; pass 0 sweeps down (sy = +1), pass 1 up
+    // (sy = -1), each into its own accumulator plane; every strip's producer
+    // is strip k - 1 of its chain (same pass and frame).  Which strip a block
+    // runs is the ticket it draws on arrival (status[2] counts the context's
+    // strip blocks, ticket0 = this launch's first), not its blockIdx: a strip
+    // only ever waits on a strip whose block arrived before it and is running
+    // or done, so the chain progresses whatever order and placement the
+    // dispatcher picks (ticket0 < 0: blockIdx order, which relies on in-order
+    // dispatch -- measured on gfx950, tools/ubench/xcc_map.hip -- and keeps a
+    // chain on one XCD under round-robin placement: strips 1.60 vs 1.68 ms).
+    __shared__ int s_ticket;
+    if (threadIdx.x == 0)
+        s_ticket = ticket0 < 0 ? (int)blockIdx.x
+                               : (int)(__hip_atomic_fetch_add((unsigned*)status + 2, 1u, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT) - (unsigned)ticket0);
+    __syncthreads();
+    const int bx = s_ticket;
+    if ((unsigned)bx >= gridDim.x) {  // ticket count out of step with the host: drain, report
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(status, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(report, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
     const int nchains = npass * nframes;
-    const int k = blockIdx.x / nchains;
-    const int chain = blockIdx.x - k * nchains;
+    const int k = bx / nchains;
+    const int chain = bx - k * nchains;
     const int pass = chain / nframes;
     const int f = chain - pass * nframes;
     const int sy = pass == 0 ? 1 : -1;
@@ -1521,7 +1541,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
 #pragma unroll
         for (int i = 0; i < NG; i++) __hip_atomic_store(q + 4 * LPC * i, g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (trace_h && lane == 0)  // MVSV_TRI_TRACE: when step t went out (100 MHz clock)
-            stats[(size_t)blockIdx.x * (8 + 2 * trace_h) + 8 + t] = __builtin_amdgcn_s_memrealtime();
+            stats[(size_t)bx * (8 + 2 * trace_h) + 8 + t] = __builtin_amdgcn_s_memrealtime();
     };
 
     // ---- compute waves ----
@@ -1564,7 +1584,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
         if (i > 0) publish(t - 1, prv);
         bconsume(t, cur, bg[j % BF]);
         if (trace_h && lane == 0)  // when the producer's step t was in
-            stats[(size_t)blockIdx.x * (8 + 2 * trace_h) + 8 + trace_h + t] = __builtin_amdgcn_s_memrealtime();
+            stats[(size_t)bx * (8 + 2 * trace_h) + 8 + trace_h + t] = __builtin_amdgcn_s_memrealtime();
         bload(t + BF, bg[j % BF]);
         __syncthreads();
     };
@@ -1708,7 +1728,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
     if (comm) {
         publish(te - 1, (len - 1) & 1);
         if (stats && lane == 0) {
-            unsigned long long* q = stats + (size_t)blockIdx.x * (8 + 2 * trace_h);
+            unsigned long long* q = stats + (size_t)bx * (8 + 2 * trace_h);
             q[0] = st_t0;
             q[1] = __builtin_amdgcn_s_memtime();
             q[2] = st_spin;
@@ -2427,9 +2447,11 @@ int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, Ac
             return rc;
     }
     if (!ctx->status.ptr) {
-        if ((rc = ensure(ctx, ctx->status, 16, "device status word"))) return rc;
+        // [0] give-up epoch, [2] strip tickets drawn
+        if ((rc = ensure(ctx, ctx->status, 16, "device status words"))) return rc;
         if ((rc = check_hip(ctx, hipMemsetAsync(ctx->status.ptr, 0, 16, ctx->stream), "status reset")))
             return rc;
+        ctx->tri_tickets = 0;
     }
     // Launch epochs never repeat between two zeroings of the granules: tag 0
     // means "never written", and when the 16-bit tag wraps every slot is
@@ -2461,8 +2483,10 @@ int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, Ac
     hipLaunchKernelGGL((sgbm_tri_kernel<NP, WV, LPC, AccT, NW>), grid, dim3(TriCfg<NP, WV, LPC>::kThreads), TL::kBytes,
                        ctx->stream, Cv, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, npass, e.P1,
                        e.P2, (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips,
-                       (int*)ctx->status.ptr, ctx->spin_limit, ctx->report_target, stats, trace_h);
+                       (int*)ctx->status.ptr, ctx->spin_limit, ctx->report_target, stats, trace_h,
+                       ctx->strip_tickets ? (long long)ctx->tri_tickets : -1ll);
     rc = check_hip(ctx, hipGetLastError(), "sgbm sheared-strip path kernel");
+    if (rc == MVSV_OK && ctx->strip_tickets) ctx->tri_tickets += grid.x;  // one ticket per block (u32 wrap is harmless)
     if (want_stats) {
         (void)hipStreamSynchronize(ctx->stream);
         std::vector<unsigned long long> h((size_t)grid.x * sb);

@@ -222,6 +222,7 @@ static void copy_options(mvsv_ctx* d, const mvsv_ctx* s)
     d->strip_waves = s->strip_waves;
     d->strip_lpc = s->strip_lpc;
     d->lines_aux = s->lines_aux;
+    d->strip_tickets = s->strip_tickets;
     d->bm2 = s->bm2;
     d->bm_ty = s->bm_ty;
 }

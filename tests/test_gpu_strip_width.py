@@ -70,3 +70,39 @@ def test_strip_width_batch_device(gpu, mvsv, oracle):
     for i, (L, R) in enumerate(pairs):
         want = oracle.sgbm(L, R, p)
         assert np.array_equal(got[i], want), f"frame {i}: " + report(got[i], want)
+
+
+@pytest.mark.parametrize("tickets", [1, 0])
+def test_strip_order_batch_device(gpu, mvsv, oracle, tickets):
+    """Strips by ticket drawn on arrival (default: no dispatch-order
+    assumption) and by blockIdx: both bit-exact on a 6-frame wide-strip
+    batch, twice in a row (the ticket counter carries over between launches)."""
+    from mvstereovision3_amd import _lib
+    torch = gpu
+    rng = np.random.default_rng(9300)
+    H, W, D = 120, 400, 64
+    pairs = [rand_pair(rng, H, W, int(rng.integers(0, 40)), k % 3) for k in range(6)]
+    m = mvsv.StereoSGBM.create(minDisparity=0, numDisparities=D, blockSize=5, P1=8, P2=32,
+                               disp12MaxDiff=1, uniquenessRatio=10, mode=1)
+    dev = torch.device("cuda", 0)
+    Lb = torch.from_numpy(np.stack([q[0] for q in pairs])).to(dev)
+    Rb = torch.from_numpy(np.stack([q[1] for q in pairs])).to(dev)
+    out = torch.empty((6, H, W), dtype=torch.int16, device=dev)
+    outs = []
+    try:
+        _lib.set_option(_lib.OPT_PATH_SCHEDULE, 1)
+        _lib.set_option(_lib.OPT_STRIP_WAVES, 15)
+        _lib.set_option(_lib.OPT_STRIP_TICKETS, tickets)
+        for _ in range(2):
+            m.compute(Lb, Rb, out)
+            outs.append(out.cpu().numpy())
+    finally:
+        _lib.set_option(_lib.OPT_STRIP_TICKETS, 1)
+        _lib.set_option(_lib.OPT_STRIP_WAVES, 0)
+        _lib.set_option(_lib.OPT_PATH_SCHEDULE, 0)
+    p = dict(min_disparity=0, num_disparities=D, block_size=5, p1=8, p2=32, disp12_max_diff=1,
+             pre_filter_cap=0, uniqueness_ratio=10, speckle_window_size=0, speckle_range=0, mode=1)
+    for i, (L, R) in enumerate(pairs):
+        want = oracle.sgbm(L, R, p)
+        for got in outs:
+            assert np.array_equal(got[i], want), f"tickets={tickets} frame {i}: " + report(got[i], want)
