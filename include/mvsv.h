@@ -106,10 +106,12 @@ enum {
      * P2 <= 15),
      * sheared strips otherwise; 1 = strips; 2 = directions side by side */
     MVSV_OPT_PATH_SCHEDULE = 4,
-    /* which strip a block of the sheared-strip kernel runs: 1 (default) = a
-     * ticket drawn on arrival, so a strip only waits on a strip already
-     * running or done whatever the dispatch order; 0 = its blockIdx (relies
-     * on in-order dispatch; keeps a strip chain on one XCD, a few % faster) */
+    /* which strip a block of the sheared-strip kernel runs in launches of
+     * more blocks than CUs: 1 (default) = a ticket drawn on arrival, so a
+     * strip only waits on a strip already running or done whatever the
+     * dispatch order; 0 = its blockIdx (relies on in-order dispatch).
+     * Launches of at most one block per CU are resident at once and always
+     * use blockIdx order. */
     MVSV_OPT_STRIP_TICKETS = 5
 };
 

@@ -74,20 +74,21 @@ def test_strip_width_batch_device(gpu, mvsv, oracle):
 
 @pytest.mark.parametrize("tickets", [1, 0])
 def test_strip_order_batch_device(gpu, mvsv, oracle, tickets):
-    """Strips by ticket drawn on arrival (default: no dispatch-order
-    assumption) and by blockIdx: both bit-exact on a 6-frame wide-strip
-    batch, twice in a row (the ticket counter carries over between launches)."""
+    """Strips by ticket drawn on arrival (default for launches of more blocks
+    than CUs: no dispatch-order assumption) and by blockIdx: both bit-exact on
+    an 8-frame wide-strip batch of 304 blocks (> 256 CUs), twice in a row (the
+    ticket counter carries over between launches)."""
     from mvstereovision3_amd import _lib
     torch = gpu
     rng = np.random.default_rng(9300)
-    H, W, D = 120, 400, 64
-    pairs = [rand_pair(rng, H, W, int(rng.integers(0, 40)), k % 3) for k in range(6)]
+    H, W, D, N = 300, 900, 64, 8  # 19 strips x 8 frames x 2 passes = 304 blocks
+    pairs = [rand_pair(rng, H, W, int(rng.integers(0, 40)), k % 3) for k in range(N)]
     m = mvsv.StereoSGBM.create(minDisparity=0, numDisparities=D, blockSize=5, P1=8, P2=32,
                                disp12MaxDiff=1, uniquenessRatio=10, mode=1)
     dev = torch.device("cuda", 0)
     Lb = torch.from_numpy(np.stack([q[0] for q in pairs])).to(dev)
     Rb = torch.from_numpy(np.stack([q[1] for q in pairs])).to(dev)
-    out = torch.empty((6, H, W), dtype=torch.int16, device=dev)
+    out = torch.empty((N, H, W), dtype=torch.int16, device=dev)
     outs = []
     try:
         _lib.set_option(_lib.OPT_PATH_SCHEDULE, 1)

@@ -13,6 +13,7 @@ cp $S/bench.json $S/configs.jsonl $S/stream_config5.json $S/valu_rate.txt $S/sq_
    $S/sq_summary.json $S/pmc_traffic.json $D/
 [ -f $S/bench_force_gather.json ] && grep '^{' $S/bench_force_gather.json > $D/bench_force_gather.json
 [ -f $S/smoke.log ] && cp $S/smoke.log $D/
+for f in c5_frame.jsonl tri_trace_c5.txt tri_trace_b8.txt xcc_map.txt; do [ -f $S/$f ] && cp $S/$f $D/; done
 [ -f $S/gpu_tests.log ] && grep -E "PASSED|FAILED|ERROR|passed|failed" $S/gpu_tests.log > $D/gpu_tests_summary.txt || true
 cp $(find $S/trace -name '*kernel_stats.csv' | head -1) $D/kernel_stats.csv
 cp $(find $S/pmc_fetch -name '*counter_collection.csv' | head -1) $D/pmc_fetch_counter_collection.csv

@@ -3,7 +3,8 @@
 # calibration), SQ/GRBM counter passes -> sq_summary.json, PMC passes
 # (FETCH_SIZE and WRITE_SIZE in separate runs) -> pmc_traffic.json, the bench
 # (reads both), the forced-gather one-rank launch, per-config table, config-5
-# stream bench, kernel-trace stats.
+# stream bench, config-5 frame probe + strip traces, dispatch-placement probe,
+# kernel-trace stats.
 # Usage (on the box, via gpurun): bash tools/gpu_round.sh TAG [--no-tests]
 set -o pipefail
 TAG=${1:-run}
@@ -35,6 +36,10 @@ cat $O/bench.json
 timeout -k 10 600 python bench.py --force-gather --no-cpu-baseline > $O/bench_force_gather.json 2> $O/bench_fg.err || { echo "force-gather bench failed"; tail -20 $O/bench_fg.err; exit 1; }
 timeout -k 10 600 python tools/bench_configs.py > $O/configs.jsonl 2> $O/configs.err || { echo "config table failed"; tail -20 $O/configs.err; exit 1; }
 timeout -k 10 300 python tools/bench_stream.py > $O/stream_config5.json 2> $O/stream.err || { echo "stream bench failed"; exit 1; }
+timeout -k 10 120 python tools/c5_frame.py > $O/c5_frame.jsonl 2>/dev/null && timeout -k 10 120 python tools/c5_frame.py --frames 2 >> $O/c5_frame.jsonl 2>/dev/null || { echo "config-5 frame probe failed"; exit 1; }
+MVSV_TRI_TRACE=$O/tri_trace_c5.bin timeout -k 10 120 python tools/c5_frame.py > /dev/null 2>&1 && python tools/tri_trace.py $O/tri_trace_c5.bin > $O/tri_trace_c5.txt || { echo "c5 strip trace failed"; exit 1; }
+MVSV_TRI_TRACE=$O/tri_trace_b8.bin timeout -k 10 120 python bench.py --no-cpu-baseline --steps 1 --warmup 0 --inflight 1 --profile-steps 0 > /dev/null 2>&1 && python tools/tri_trace.py $O/tri_trace_b8.bin > $O/tri_trace_b8.txt || { echo "batch strip trace failed"; exit 1; }
+timeout -k 10 60 ./tools/ubench/xcc_map 576 20 > $O/xcc_map.txt 2>&1 || { echo "xcc probe failed"; exit 1; }
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 10 --inflight 1 > $O/trace.log 2>&1 || { echo "trace failed"; exit 1; }
 echo "round ok"
