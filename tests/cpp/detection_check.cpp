@@ -57,6 +57,20 @@ int main(int argc, char** argv)
             if (std::memcmp(d1.ptr<int16_t>(y), direct.ptr<int16_t>(y), 640) ||
                 std::memcmp(d2.ptr<int16_t>(y), direct.ptr<int16_t>(y), 640))
                 return 5;
+        // two frame-batch launches in flight on the stream's compute lanes
+        {
+            mvsv::DisparityStream st2(*sgbm, 320, 96, 4, &roi_u);
+            st2.setInflight(2);
+            for (int i = 0; i < 4; i++) st2.push(s);
+            for (int i = 0; i < 4; i++) {
+                mvsv::Mat di;
+                float gi[81];
+                st2.pop(di, gi);
+                for (int y = 0; y < 96; y++)
+                    if (std::memcmp(di.ptr<int16_t>(y), direct.ptr<int16_t>(y), 640)) return 7;
+                if (std::memcmp(gi, g1, sizeof(gi))) return 8;
+            }
+        }
         mvsv::MeanDisparityDetection m2(dir);
         mvsv::Mat w2 = direct(roi_u);
         m2.init(w2, Q, 0.1f, 1.5f);

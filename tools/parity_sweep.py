@@ -1,6 +1,6 @@
 """Randomized parity sweep (GPU box): many random StereoSGBM / StereoBM cases --
 shapes, parameters, OpenCV variants, frame batches and every launch-shape option
-(SGBM path schedule, strip width; BM tile rows, general kernel) -- computed on the
+(SGBM path schedule, strip width, strip order; BM tile rows, general kernel) -- computed on the
 GPU through the package and checked bit-exactly against the C oracle (test
 infrastructure; the oracle frames run on a process pool of host threads).
 
@@ -78,6 +78,7 @@ def main():
         m.setVariant(variant)
         _lib.set_option(_lib.OPT_PATH_SCHEDULE, sched)
         _lib.set_option(_lib.OPT_STRIP_WAVES, waves)
+        _lib.set_option(_lib.OPT_STRIP_TICKETS, int(rng.integers(0, 2)))
         try:
             if n == 1:
                 got = m.compute(*pairs[0])[None]
@@ -108,6 +109,9 @@ def main():
                   preFilterCap=int(rng.choice([0, 31, 63])), uniquenessRatio=int(rng.choice([0, 10])),
                   speckleWindowSize=int(rng.choice([0, 150])), speckleRange=2, mode=int(rng.integers(0, 2)))
         m = mvsv.StereoSGBM.create(**kw)
+        tickets = int(rng.integers(0, 2))  # strip order of launches larger than the CU count
+        _lib.set_option(_lib.OPT_STRIP_TICKETS, tickets)
+        kw["strip_tickets"] = tickets
         pairs = [mvsv.synth_pair(int(rng.integers(0, 1 << 30)), W, H, max(kw["minDisparity"], 0), D)
                  for _ in range(n)]
         Lb = torch.from_numpy(np.stack([q[0] for q in pairs])).to(dev)
@@ -118,6 +122,7 @@ def main():
         p = {k: v for k, v in m.params().items() if k != "variant"}
         for j, (L, R) in enumerate(pairs):
             jobs.append((f"large #{i} frame {j}/{n} {W}x{H} {kw}", got[j], pool.submit(pyoracle.sgbm, L, R, p)))
+    _lib.set_option(_lib.OPT_STRIP_TICKETS, 1)
 
     for i in range(a.bm):
         H, W = int(rng.integers(24, 200)), int(rng.integers(80, 400))
