@@ -272,6 +272,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
         if (std::strstr(v, "path-wave")) c->path16 = 0;
         if (std::strstr(v, "path-lines")) c->tri = 0;
         if (std::strstr(v, "bm-tile")) c->bm2 = 0;
+        if (std::strstr(v, "cost-generic")) c->cost_fixed_pp = 0;
     }
     if (const char* v = std::getenv("MVSV_COST_TY")) c->cost_ty = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("MVSV_PATH_SCHEDULE")) c->path_sched = std::max(0, std::min(2, std::atoi(v)));

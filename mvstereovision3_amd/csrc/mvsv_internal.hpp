@@ -117,6 +117,7 @@ struct mvsv_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int path16 = 1;  // 16-lanes-per-scanline path kernels where D allows
     int cost2 = 1;   // register-ring cost kernel where blockSize <= 15
+    int cost_fixed_pp = 1;  // fixed-pair-count cost kernels for D = 128 / 256 (MVSV_KERNELS=cost-generic: off)
     int cost_ty = 0;  // cost-volume tile height (0 = by image height); MVSV_COST_TY for A/B runs
     int tri = 1;     // sheared-strip kernels: three directions per sweep
     int path_sched = 0;   // 16-lane path schedule: 0 = by launch size, 1 = strips, 2 = directions side by side

@@ -2772,6 +2772,30 @@ int launch_paths_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
 
 }  // namespace
 
+using Cost2Kern = void (*)(const uint64_t*, int, int, SgbmEff, int, int16_t*);
+template <int STG, int PPC>
+static Cost2Kern cost2_pick_nr(int nr)
+{
+    switch (nr) {
+    case 1: return sgbm_cost2_kernel<1, STG, PPC>;
+    case 3: return sgbm_cost2_kernel<3, STG, PPC>;
+    case 5: return sgbm_cost2_kernel<5, STG, PPC>;
+    case 7: return sgbm_cost2_kernel<7, STG, PPC>;
+    case 9: return sgbm_cost2_kernel<9, STG, PPC>;
+    case 11: return sgbm_cost2_kernel<11, STG, PPC>;
+    case 13: return sgbm_cost2_kernel<13, STG, PPC>;
+    default: return sgbm_cost2_kernel<15, STG, PPC>;
+    }
+}
+// kernel for blockSize nr, STG staged items per thread (1 / 2), PPC pairs (64 /
+// 128 fixed, 0 = from the layout)
+static Cost2Kern cost2_pick(int nr, int stg, int ppc)
+{
+    if (stg == 1)
+        return ppc == 64 ? cost2_pick_nr<1, 64>(nr) : ppc == 128 ? cost2_pick_nr<1, 128>(nr) : cost2_pick_nr<1, 0>(nr);
+    return ppc == 64 ? cost2_pick_nr<2, 64>(nr) : ppc == 128 ? cost2_pick_nr<2, 128>(nr) : cost2_pick_nr<2, 0>(nr);
+}
+
 // Cost-volume launch: the register-ring kernel when blockSize <= 15 and the
 // tile fits, else the LDS-ring kernel.
 static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int TY,
@@ -2786,32 +2810,12 @@ static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int
         if (l2.CL >= 1 && items <= kCost2Threads * 2 &&
             l2.bytes <= 160 * 1024) {
             dim3 grid2((e.W1 + l2.TX - 1) / l2.TX, (H + TY - 1) / TY, n);
-            void (*kern)(const uint64_t*, int, int, SgbmEff, int, int16_t*) = nullptr;
+            Cost2Kern kern = nullptr;
             const bool two = items > kCost2Threads;
-            const bool pp64 = l2.PP == 64;
-            if (!two) {
-                switch (2 * e.SH2 + 1) {
-                case 1: kern = pp64 ? sgbm_cost2_kernel<1, 1, 64> : sgbm_cost2_kernel<1, 1, 0>; break;
-                case 3: kern = pp64 ? sgbm_cost2_kernel<3, 1, 64> : sgbm_cost2_kernel<3, 1, 0>; break;
-                case 5: kern = pp64 ? sgbm_cost2_kernel<5, 1, 64> : sgbm_cost2_kernel<5, 1, 0>; break;
-                case 7: kern = pp64 ? sgbm_cost2_kernel<7, 1, 64> : sgbm_cost2_kernel<7, 1, 0>; break;
-                case 9: kern = pp64 ? sgbm_cost2_kernel<9, 1, 64> : sgbm_cost2_kernel<9, 1, 0>; break;
-                case 11: kern = pp64 ? sgbm_cost2_kernel<11, 1, 64> : sgbm_cost2_kernel<11, 1, 0>; break;
-                case 13: kern = pp64 ? sgbm_cost2_kernel<13, 1, 64> : sgbm_cost2_kernel<13, 1, 0>; break;
-                default: kern = pp64 ? sgbm_cost2_kernel<15, 1, 64> : sgbm_cost2_kernel<15, 1, 0>; break;
-                }
-            } else {
-                switch (2 * e.SH2 + 1) {
-                case 1: kern = pp64 ? sgbm_cost2_kernel<1, 2, 64> : sgbm_cost2_kernel<1, 2, 0>; break;
-                case 3: kern = pp64 ? sgbm_cost2_kernel<3, 2, 64> : sgbm_cost2_kernel<3, 2, 0>; break;
-                case 5: kern = pp64 ? sgbm_cost2_kernel<5, 2, 64> : sgbm_cost2_kernel<5, 2, 0>; break;
-                case 7: kern = pp64 ? sgbm_cost2_kernel<7, 2, 64> : sgbm_cost2_kernel<7, 2, 0>; break;
-                case 9: kern = pp64 ? sgbm_cost2_kernel<9, 2, 64> : sgbm_cost2_kernel<9, 2, 0>; break;
-                case 11: kern = pp64 ? sgbm_cost2_kernel<11, 2, 64> : sgbm_cost2_kernel<11, 2, 0>; break;
-                case 13: kern = pp64 ? sgbm_cost2_kernel<13, 2, 64> : sgbm_cost2_kernel<13, 2, 0>; break;
-                default: kern = pp64 ? sgbm_cost2_kernel<15, 2, 64> : sgbm_cost2_kernel<15, 2, 0>; break;
-                }
-            }
+            // numDisparities 128 / 256: the pair count is a compile-time
+            // constant (unrolled pixel-cost loop, immediate LDS offsets)
+            const int ppc = !ctx->cost_fixed_pp ? 0 : l2.PP == 64 ? 64 : (l2.PP == 128 ? 128 : 0);
+            kern = cost2_pick(2 * e.SH2 + 1, two ? 2 : 1, ppc);
             if (l2.bytes > 65536 &&
                 (rc = check_hip(ctx, hipFuncSetAttribute((const void*)kern,
                                                          hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -216,6 +216,7 @@ static void copy_options(mvsv_ctx* d, const mvsv_ctx* s)
     d->spin_limit = s->spin_limit;
     d->path16 = s->path16;
     d->cost2 = s->cost2;
+    d->cost_fixed_pp = s->cost_fixed_pp;
     d->cost_ty = s->cost_ty;
     d->tri = s->tri;
     d->path_sched = s->path_sched;
