@@ -82,7 +82,7 @@ def parse(argv=None):
     ap.add_argument("--inflight", type=int, default=2,
                     help="batches in flight: consecutive steps on separate HIP streams / contexts "
                          "(their kernels overlap); 1 = strictly one step after the other")
-    ap.add_argument("--profile-steps", type=int, default=10,
+    ap.add_argument("--profile-steps", type=int, default=200,
                     help="steps of the separate one-in-flight pass that times the stages (roofline)")
     ap.add_argument("--force-gather", action="store_true",
                     help="run the multi-rank path even for --gpus 1: torch.distributed.run "
