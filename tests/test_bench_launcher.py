@@ -4,6 +4,8 @@ launcher and the int16-as-bytes gather on CPU with gloo (trivial host compute,
 no GPU): the gathered global batch must hold every rank's frames in order."""
 import json
 import os
+
+import pytest
 import subprocess
 import sys
 
@@ -18,15 +20,16 @@ def _run(args, env_extra=None):
                           capture_output=True, text=True, timeout=240)
 
 
-def test_bench_spawns_ranks_and_gathers():
-    r = _run(["--dry", "--gpus", "2", "--width", "96", "--height", "48", "--frames", "2",
+@pytest.mark.parametrize("n", [2, 4, 8])  # the driver's scaling sweep shapes (N = 1 is the GPU bench)
+def test_bench_spawns_ranks_and_gathers(n):
+    r = _run(["--dry", "--gpus", str(n), "--width", "96", "--height", "48", "--frames", "2",
               "--steps", "1", "--warmup", "0"])
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     res = json.loads(lines[0])
-    assert res["n_gpus"] == 2 and res["global_batch"] == 4 and res["gather"] == "gloo"
-    assert res["gathered_frames_ok"] == "4/4"
+    assert res["n_gpus"] == n and res["global_batch"] == 2 * n and res["gather"] == "gloo"
+    assert res["gathered_frames_ok"] == f"{2 * n}/{2 * n}"
 
 
 def test_bench_rejects_world_size_mismatch():
