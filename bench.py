@@ -54,7 +54,7 @@ if ROOT not in sys.path:
 SEED0 = 0x5EED0000
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SGBM_YML = os.path.join(ROOT, "tests", "golden", "configs", "sgbm.yml")
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
 PMC_FILE = os.path.join(PROFILE_DIR, "pmc_traffic.json")  # tools/pmc_traffic.py
 SQ_FILE = os.path.join(PROFILE_DIR, "sq_summary.json")    # tools/sq_summary.py
 KERNEL_SOURCES = os.path.join(ROOT, "mvstereovision3_amd", "csrc")
@@ -87,6 +87,8 @@ def parse(argv=None):
     ap.add_argument("--force-gather", action="store_true",
                     help="run the multi-rank path even for --gpus 1: torch.distributed.run "
                          "child, NCCL (RCCL) process group, dist.gather of the maps every step")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the per-config table (BASELINE configs 1, 2, 3, 5; single GPU only)")
     ap.add_argument("--dry", action="store_true",
                     help="CPU rehearsal of launcher + gather (gloo, trivial compute)")
     return ap.parse_args(argv)
@@ -117,23 +119,26 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True):
+def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True, res=False):
     """Implementation HBM bytes of one step per stage ("Kernels").
 
     acc = bytes per (pixel, disparity) of a path-delta accumulator plane (0.5 for
     the 4-bit planes of the strip schedule when 3 * P2 <= 15, 1 when
     ndir * P2 <= 255, else 2).  strips = the sheared-strip schedule (D in
     {32, 64, 128, 256}): the strip kernel runs npass passes (down, + up for 8
-    paths) that each read C and write their own plane, the L->R line kernel
-    reads C and writes a plane, the final kernel reads C and every plane.
+    paths) that each read their cost input and write their own plane, the L->R
+    line kernel reads its cost input and writes a plane, the final kernel reads C
+    and every plane.  res = the direction passes read the nibble cost residual
+    plane (0.5 B per cost, written by the cost kernel beside C) instead of C.
     """
     cells = W1 * H * D
     px = W * H
     npass = 2 if ndir == 8 else 1
+    cin = 0.5 if res else 2
     if strips:
         planes = npass + 1
-        strip_b = F * cells * npass * (2 + acc)
-        lines_b = F * cells * (2 + acc)
+        strip_b = F * cells * npass * (cin + acc)
+        lines_b = F * cells * (cin + acc)
         path_b = strip_b + lines_b
         final_b = F * (cells * (2 + planes * acc) + 2 * px)
     else:
@@ -142,7 +147,7 @@ def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True):
         final_b = F * (cells * (2 + acc) + 2 * px)
     return {
         "prefilter": F * (2 * px + 2 * 8 * px),
-        "cost_volume": F * (2 * 8 * px + 2 * cells),
+        "cost_volume": F * (2 * 8 * px + (2 + (0.5 if res else 0)) * cells),
         "cost_fixup": 0,
         "path_aggregation": path_b,
         "path_strips": strip_b,
@@ -174,6 +179,123 @@ def kernel_source_sha() -> str:
                     glob.glob(os.path.join(KERNEL_SOURCES, "*.hpp"))):
         h.update(open(p, "rb").read())
     return h.hexdigest()[:16]
+
+
+VALU_INT16_PEAK_TOPS = 157.3  # packed int16 ops/s x 1e-12 (2 x 78.6 T lane-ops/s)
+OPS_PER_PXD = {"sgbm5": 50, "bm": 7}  # SURVEY.md §8(d) int16 ops per (pixel, disparity)
+
+
+def config_table(mvsv, _lib, dev, steps=10, warmup=3):
+    """The other BASELINE configs on this GPU: device-resident
+    HIP-event median of `steps` steps after `warmup`, each with the roof SURVEY.md
+    §8(d) quotes it against (HBM on 4*W*H*(1+D) bytes for 8 paths, VALU on its
+    int16 op count for 5 paths and StereoBM) and a parity flag -- frame 0 of the
+    output against the oracle, computed after all timing (oracles in threads)."""
+    import numpy as np
+    import torch
+    from oracle import pyoracle
+
+    cfg = os.path.join(ROOT, "tests", "golden", "configs")
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize(dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        ev[0].record()
+        for i in range(steps):
+            fn()
+            ev[i + 1].record()
+        torch.cuda.synchronize(dev)
+        return statistics.median(ev[i].elapsed_time(ev[i + 1]) for i in range(steps))
+
+    def frames(n, W, H, minD, D):
+        pairs = [mvsv.synth_pair(SEED0 + i, W, H, minD, D) for i in range(n)]
+        L = torch.from_numpy(np.stack([q[0] for q in pairs])).to(dev)
+        R = torch.from_numpy(np.stack([q[1] for q in pairs])).to(dev)
+        return pairs, L, R
+
+    recs, checks = {}, []
+
+    def add(name, W, H, D, n, ms, roof, pair, out0, oracle_fn, extra=None):
+        t = ms / 1e3
+        rec = {"width": W, "height": H, "num_disparities": D, "frames": n, "median_ms": round(ms, 4),
+               "mpix_s": round(W * H * n / t / 1e6, 1)}
+        kind, amount = roof
+        if kind == "hbm":
+            rec["roof"] = {"bound": "hbm", "achieved_GBps": round(amount / t / 1e9, 1),
+                           "frac": round(amount / t / (HBM_PEAK_GBPS * 1e9), 4),
+                           "model": "4*W*H*(1+D) bytes per frame"}
+        else:
+            rec["roof"] = {"bound": "valu", "achieved_Tops": round(amount / t / 1e12, 2),
+                           "frac": round(amount / t / (VALU_INT16_PEAK_TOPS * 1e12), 4),
+                           "model": f"{OPS_PER_PXD[kind]} int16 ops per (pixel, disparity)"}
+        rec.update(extra or {})
+        recs[name] = rec
+        checks.append((name, pair, out0, oracle_fn))
+
+    # configs 1-2: StereoBM 640x480 (configs/bm.yml; StereoBM(64, 9) OpenCV defaults)
+    for name, D in (("config1_bm_yml_640x480", 80), ("config2_bm_d64_bs9_640x480", 64)):
+        if D == 80:
+            b = mvsv.StereoBM.create(0, 21)
+            assert mvsv.Disparity.loadBMParameters(os.path.join(cfg, "bm.yml"), b)
+        else:
+            b = mvsv.StereoBM.create(64, 9)
+        bp = b.params()
+        for n in ((8,) if D == 80 else (1, 8)):
+            pairs, L, R = frames(n, 640, 480, 0, D)
+            out = torch.empty((n, 480, 640), dtype=torch.int16, device=dev)
+            ctx = _lib.context(dev.index or 0)
+            _lib.profile_reset(ctx)
+            _lib.profile_enable(ctx, True)
+            ms = timed(lambda: b.compute(L, R, out))
+            _lib.profile_enable(ctx, False)
+            bm_ms, bm_n = _lib.profile_read(ctx).get("bm_match", (0.0, 0))
+            add(f"{name}_batch{n}", 640, 480, D, n, ms, ("bm", OPS_PER_PXD["bm"] * 640 * 480 * D * n),
+                pairs[0], out[0].cpu().numpy(), lambda L0, R0, bp=bp: pyoracle.bm(L0, R0, bp),
+                {"bm_match_kernel_ms": round(bm_ms / max(bm_n, 1), 4)})
+    # config 3: SGBM configs/sgbm.yml 640x480, one frame (the live-camera case), 5 and 8 paths
+    for mode in (0, 1):
+        m = mvsv.StereoSGBM.create(0, 0, 0, 0, 0)
+        assert mvsv.Disparity.loadSGBMParameters(os.path.join(cfg, "sgbm.yml"), m, mvsv.sgbmParameters())
+        m.setMode(mode)
+        p = {k: v for k, v in m.params().items() if k != "variant"}
+        pairs, L, R = frames(1, 640, 480, 1, 128)
+        out = torch.empty((1, 480, 640), dtype=torch.int16, device=dev)
+        ms = timed(lambda: m.compute(L, R, out))
+        roof = ("hbm", 4 * 640 * 480 * 129) if mode else ("sgbm5", OPS_PER_PXD["sgbm5"] * 640 * 480 * 128)
+        add(f"config3_sgbm_yml_640x480_{'8path' if mode else '5path'}_batch1", 640, 480, 128, 1, ms, roof,
+            pairs[0], out[0].cpu().numpy(), lambda L0, R0, p=p: pyoracle.sgbm(L0, R0, p),
+            {"mode": "MODE_HH" if mode else "MODE_SGBM"})
+    # config 5: liveDisparity's create(0, 256, 9, 648, 2592) (trgt/liveDisparity.cpp:61,
+    # MODE_SGBM, no speckle) at 1280x960: one frame and the stream's batch of 8
+    m256 = mvsv.StereoSGBM.create(0, 256, 9, 648, 2592)
+    p256 = {k: v for k, v in m256.params().items() if k != "variant"}
+    for n in (1, 8):
+        pairs, L, R = frames(n, 1280, 960, 0, 256)
+        out = torch.empty((n, 960, 1280), dtype=torch.int16, device=dev)
+        ms = timed(lambda: m256.compute(L, R, out))
+        add(f"config5_sgbm_1280x960_d256_batch{n}", 1280, 960, 256, n, ms,
+            ("sgbm5", OPS_PER_PXD["sgbm5"] * 1280 * 960 * 256 * n), pairs[0], out[0].cpu().numpy(),
+            (lambda L0, R0, p=p256: pyoracle.sgbm(L0, R0, p)) if n == 1 else None, {"mode": "MODE_SGBM"})
+    # parity: frame 0 of every config against the oracle (outside all timing; the
+    # batch-8 config-5 line shares frame 0's seed with the batch-1 line, checked once)
+    pyoracle.lib()
+    verdict = {}
+
+    def work(item):
+        name, (L0, R0), got, fn = item
+        if fn is not None:
+            verdict[name] = bool(np.array_equal(got, fn(L0, R0)))
+
+    ts = [threading.Thread(target=work, args=(c,)) for c in checks]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for name, rec in recs.items():
+        rec["parity_frame0"] = verdict.get(name, verdict.get(name.replace("batch8", "batch1")))
+    return recs
 
 
 def cpu_info():
@@ -310,6 +432,12 @@ def main(argv=None):
     # bytes per (pixel, disparity) of an accumulator plane: 4-bit planes on the
     # strip schedule when 3 * P2 <= 15 (sgbm.yml: P2 = 5), else u8 / u16
     acc = 0.5 if (D in (32, 64, 128, 256) and 3 * P2 <= 15) else (1 if ndir * P2 <= 255 else 2)
+    # the cost residual plane (mvsv.h MVSV_OPT_COST_RESIDUAL): no-wrap bound,
+    # 3 * P2 <= 15, D <= 128 -- sgbm.yml
+    bs = params["block_size"] if params["block_size"] > 0 else 5
+    ftzero = max(params["pre_filter_cap"], 15) | 1
+    residual = (os.environ.get("MVSV_COST_RESIDUAL", "1") != "0" and D in (32, 64, 128) and 3 * P2 <= 15
+                and 2 * P2 + bs * bs * (2 * ftzero + 63) <= 32767)
 
     from mvstereovision3_amd.batch import FrameBatch, InflightBatches, frame_seeds
     host = [mvsv.synth_pair(sd, W, H, minD, D) for sd in frame_seeds(rank, world, F, SEED0)]
@@ -404,7 +532,7 @@ def main(argv=None):
         comp = 4 * W * H * (1 + D)
         alg_bytes_per_launch = comp * F / launches
         achieved = alg_bytes_per_launch / avg_launch_s / 1e9
-        impl_bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir, acc, strips) / launches
+        impl_bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir, acc, strips, residual) / launches
         workload = f"sgbm_{W}x{H}_d{D}_{ndir}path_batch{F}"
         sha = kernel_source_sha()
         pmc, traffic_note = _summary(PMC_FILE, workload, sha, "PMC")
@@ -490,6 +618,12 @@ def main(argv=None):
                                    "latency_1core_s": round(lat, 3),
                                    "host": info}
             res["parity_sample"] = f"{same}/{nchk} frames bit-exact vs oracle"
+        if world == 1 and not args.no_configs and not distributed:
+            tc0 = time.perf_counter()
+            res["configs"] = config_table(mvsv, _lib, dev)
+            res["configs_note"] = (f"BASELINE configs 1, 2, 3, 5 on this GPU, device-resident (median of 10 "
+                                   f"HIP-event steps after 3 warm-up), roof per SURVEY.md §8(d), parity_frame0 = "
+                                   f"frame 0 vs the oracle; {time.perf_counter() - tc0:.1f} s incl. oracles")
         if gathered is not None:
             # the gathered global batch: frame 0 of every rank, as it arrived on
             # rank 0, against the oracle (outside the timed region)

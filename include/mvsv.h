@@ -106,13 +106,18 @@ enum {
      * P2 <= 15),
      * sheared strips otherwise; 1 = strips; 2 = directions side by side */
     MVSV_OPT_PATH_SCHEDULE = 4,
-    /* which strip a block of the sheared-strip kernel runs in launches of
-     * more blocks than CUs: 1 (default) = a ticket drawn on arrival, so a
-     * strip only waits on a strip already running or done whatever the
-     * dispatch order; 0 = its blockIdx (relies on in-order dispatch).
-     * Launches of at most one block per CU are resident at once and always
-     * use blockIdx order. */
-    MVSV_OPT_STRIP_TICKETS = 5
+    /* which strip a block of the sheared-strip kernel runs: 1 (default) = a
+     * ticket drawn on arrival, so a strip only waits on a strip already
+     * running or done whatever the dispatch order and whatever else shares
+     * the GPU (every launch size); 0 = its blockIdx (relies on in-order
+     * dispatch, A/B runs only). */
+    MVSV_OPT_STRIP_TICKETS = 5,
+    /* SGBM direction passes read the cost residual plane
+     * R = min(C - min_d C, 2*P2) + P2 (one nibble per cost, 4x fewer bytes
+     * than C) instead of C where that is exact: no int16 wrap is possible,
+     * 3*P2 <= 15 and numDisparities <= 128 (configs/sgbm.yml).  1 (default)
+     * = on, 0 = always read C (A/B runs); results are identical either way. */
+    MVSV_OPT_COST_RESIDUAL = 6
 };
 
 /* StereoSGBM modes (cv::StereoSGBM::MODE_SGBM / MODE_HH). */

@@ -30,6 +30,7 @@ OPT_BM_TILE_ROWS = 2
 OPT_STRIP_WAVES = 3
 OPT_PATH_SCHEDULE = 4
 OPT_STRIP_TICKETS = 5
+OPT_COST_RESIDUAL = 6
 
 MODE_SGBM = 0
 MODE_HH = 1

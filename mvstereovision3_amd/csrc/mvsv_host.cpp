@@ -277,7 +277,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
     if (const char* v = std::getenv("MVSV_COST_TY")) c->cost_ty = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("MVSV_PATH_SCHEDULE")) c->path_sched = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("MVSV_STRIP_WAVES")) c->strip_waves = std::max(0, std::atoi(v));
-    if (const char* v = std::getenv("MVSV_STRIP_LPC")) c->strip_lpc = std::atoi(v) == 8 ? 8 : 16;
+    if (const char* v = std::getenv("MVSV_COST_RESIDUAL")) c->cost_res = std::atoi(v) != 0;
     if (const char* v = std::getenv("MVSV_BM_TY")) c->bm_ty = std::max(0, std::min(128, std::atoi(v)));
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess) {
         (void)hipGetLastError();
@@ -301,7 +301,7 @@ int mvsv_trim(mvsv_ctx* ctx)
     if (!ctx) return MVSV_E_INVALID_ARG;
     DeviceGuard dev_guard(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    DevBuf* all[] = {&ctx->pre, &ctx->cost, &ctx->agg, &ctx->raw, &ctx->uf_parent, &ctx->uf_size,
+    DevBuf* all[] = {&ctx->pre, &ctx->cost, &ctx->cres, &ctx->agg, &ctx->raw, &ctx->uf_parent, &ctx->uf_size,
                      &ctx->uf_tile, &ctx->tri_bnd, &ctx->status,
                      &ctx->dummy, &ctx->keys,
                      &ctx->bm_lf, &ctx->bm_rf, &ctx->bm_cost, &ctx->bm_sad, &ctx->h_left, &ctx->h_right,
@@ -431,6 +431,10 @@ int mvsv_set_option(mvsv_ctx* ctx, int option, long long value)
     case MVSV_OPT_STRIP_TICKETS:
         if (value < 0 || value > 1) return set_error(ctx, MVSV_E_INVALID_ARG, "strip tickets must be 0 or 1");
         ctx->strip_tickets = (int)value;
+        return MVSV_OK;
+    case MVSV_OPT_COST_RESIDUAL:
+        if (value < 0 || value > 1) return set_error(ctx, MVSV_E_INVALID_ARG, "cost residual must be 0 or 1");
+        ctx->cost_res = (int)value;
         return MVSV_OK;
     default:
         return set_error(ctx, MVSV_E_INVALID_ARG, "unknown option");

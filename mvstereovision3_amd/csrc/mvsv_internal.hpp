@@ -89,7 +89,7 @@ struct mvsv_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // SGBM
-    mvsv::DevBuf pre, cost, agg, raw, uf_parent, uf_size, uf_tile, dummy, keys, tri_bnd, status;
+    mvsv::DevBuf pre, cost, cres, agg, raw, uf_parent, uf_size, uf_tile, dummy, keys, tri_bnd, status;
     // launch number of the last sheared-strip launch: its low 16 bits tag the
     // boundary granules (tri_bnd is re-zeroed whenever they wrap), all 32 bits
     // go into status[0] when that launch gives up a wait (no per-call reset)
@@ -122,7 +122,7 @@ struct mvsv_ctx {
     int tri = 1;     // sheared-strip kernels: three directions per sweep
     int path_sched = 0;   // 16-lane path schedule: 0 = by launch size, 1 = strips, 2 = directions side by side
     int strip_waves = 0;  // compute waves per strip (0 = by launch size; 4 or the wide count forces)
-    int strip_lpc = 16;   // lanes per strip column for D = 128: 16, or 8 (16 disparities per lane)
+    int cost_res = 1;     // direction passes read the cost residual plane where exact (MVSV_OPT_COST_RESIDUAL)
     int lines_aux = -1;  // L->R line kernel beside the strip kernel: -1 = small launches only, 0 / 1 / 2 force
     int bm2 = 1;     // StereoBM: disparities-on-lanes match kernel where blockSize <= 21, D <= 128
     int bm_ty = 0;   // its tile height (0 = chosen per launch); MVSV_BM_TY for A/B runs

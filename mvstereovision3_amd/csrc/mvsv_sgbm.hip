@@ -160,6 +160,50 @@ __device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b)
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
 }
 
+// Two independent u16 minima over each 16-lane row (packed in one dword).
+__device__ __forceinline__ uint32_t row_min_u16x2(uint32_t v)
+{
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, false));
+    return v;
+}
+
+// ... over aligned segments of `lanes` = 16, 32 or 64 lanes (wave-uniform):
+// the row butterfly, then rows (0,1) / (2,3) joined by v_permlane16_swap and the
+// two halves by v_permlane32_swap; every lane of a segment gets its minima.
+__device__ __forceinline__ uint32_t seg_min_u16x2(uint32_t v, int lanes)
+{
+    v = row_min_u16x2(v);
+    if (lanes >= 32) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        v = pk_min_u16(sw[0], sw[1]);
+    }
+    if (lanes >= 64) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        v = pk_min_u16(sw[0], sw[1]);
+    }
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// Residual cost plane R (the "cost residual"): for every pixel p and disparity
+//     R(p, d) = min(C(p, d) - min_k C(p, k), 2*P2) + P2        in [P2, 3*P2]
+// stored as nibbles (byte k of a pixel = R(2k) | R(2k+1) << 4; 3*P2 <= 15).
+// Why the direction passes may read R instead of C (exactly, bit for bit):
+//  * offset: a path step subtracts min_k L(prev, k) and only uses
+//    L(prev, .) - min L(prev, .), so adding a constant to C(p, .) for all d
+//    changes no path delta (and every L stays an exact non-negative int16 in
+//    the no-wrap regime the launcher requires, sgbm_no_wrap);
+//  * clamp: a step only sees min(L(prev, d) - min L(prev, .), P2) (the P2
+//    candidate caps every term), and with C' = C - min_k C, min L(prev, .) <=
+//    P2 (the d with C' = 0 has L <= C' + P2), so any C'(d) >= 2*P2 gives
+//    L(d) - min L >= P2 whatever its exact value -- and never attains min L.
+// The path-delta planes computed from R are therefore identical to those from
+// C; the final kernel (WTA, uniqueness ratio, sub-pixel fit) still reads C.
+// ---------------------------------------------------------------------------
+
 // BT cost of one channel for a disparity pair: u* broadcast, v* per half.
 __device__ __forceinline__ uint32_t bt_pair(uint32_t u, uint32_t u0, uint32_t u1, uint32_t v,
                                            uint32_t v0, uint32_t v1)
@@ -346,7 +390,8 @@ __device__ __forceinline__ uint32_t bt_cost2(uint4 u4, uint2 u2, uint4 v4, uint2
 template <int NR, int STG, int PPC>
 __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4))) void sgbm_cost2_kernel(const uint64_t* __restrict__ pre,
                                                                    int W, int H, SgbmEff e, int TY,
-                                                                   int16_t* __restrict__ C)
+                                                                   int16_t* __restrict__ C,
+                                                                   uint8_t* __restrict__ Rv)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int SH2 = NR / 2;
@@ -554,13 +599,36 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                 const int yo = y0 - 2 * SH2 + k;
                 const bool pin_row = hh_pin && yo >= ybot;
                 const bool pin_x0 = hh_pin && !fix_x0 && yo >= 1 && x0 + tx0 == 0;
+                uint32_t ov[kCost2Run];
 #pragma unroll
                 for (int i = 0; i < kCost2Run; i++) {
                     if (i > 0) h = pk_sub_u16(pk_add_u16(h, wv[i + NR - 1]), wv[i - 1]);
                     csum[i] = pk_add_u16(pk_sub_u16(csum[i], ring[s][i]), h);
                     ring[s][i] = h;
                     const bool pin = pin_row || (i == 0 && pin_x0);
-                    if (emit && i < nout) orow[i * PP] = pin ? p2x2 : pk_add_u16(p2x2, csum[i]);
+                    ov[i] = pin ? p2x2 : pk_add_u16(p2x2, csum[i]);
+                    if (emit && i < nout) orow[i * PP] = ov[i];
+                }
+                // residual plane: the lanes of a column lane hold its pixel's
+                // D costs (PP <= 64 lanes, one aligned segment of the wave);
+                // the four columns' minima in two packed segment reductions
+                if (Rv && emit) {
+                    const uint32_t m01 = seg_min_u16x2(
+                        pk_min_u16(__builtin_amdgcn_perm(ov[1], ov[0], 0x05040100u),
+                                   __builtin_amdgcn_perm(ov[1], ov[0], 0x07060302u)), PP);
+                    const uint32_t m23 = seg_min_u16x2(
+                        pk_min_u16(__builtin_amdgcn_perm(ov[3], ov[2], 0x05040100u),
+                                   __builtin_amdgcn_perm(ov[3], ov[2], 0x07060302u)), PP);
+                    const uint32_t mm[kCost2Run] = {
+                        __builtin_amdgcn_perm(m01, m01, 0x01000100u), __builtin_amdgcn_perm(m01, m01, 0x03020302u),
+                        __builtin_amdgcn_perm(m23, m23, 0x01000100u), __builtin_amdgcn_perm(m23, m23, 0x03020302u)};
+                    uint8_t* rrow = Rv + (orow - (uint32_t*)C);  // byte (pixel, pair) = dword (pixel, pair) of C
+                    const uint32_t p2x4 = pk_add_u16(p2x2, p2x2);
+#pragma unroll
+                    for (int i = 0; i < kCost2Run; i++) {
+                        const uint32_t r = pk_add_u16(pk_min_u16(pk_sub_u16(ov[i], mm[i]), p2x4), p2x2);
+                        if (i < nout) rrow[i * PP] = (uint8_t)(r | (r >> 12));
+                    }
                 }
             }
         }
@@ -572,8 +640,10 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
 //    recomputed (MODE_SGBM keeps the last computed row, MODE_HH keeps P2).
 // Column x = 0 of rows 1 .. ybot - 1 (block per row; not launched with
 // FIRSTCOL_FIX): C(0, 0, d), or P2 in MODE_HH.
+// A pixel's residual (when Rv != nullptr) depends only on its own D costs, so
+// a copied cost vector carries its residual bytes along (P2 everywhere: P2).
 __global__ __launch_bounds__(256) void sgbm_cost_fixup_col0_kernel(int16_t* __restrict__ C, int H,
-                                                                   SgbmEff e)
+                                                                   SgbmEff e, uint8_t* __restrict__ Rv)
 {
     const int y = 1 + blockIdx.x;
     const int f = blockIdx.y;
@@ -581,13 +651,20 @@ __global__ __launch_bounds__(256) void sgbm_cost_fixup_col0_kernel(int16_t* __re
     int16_t* Cf = C + (size_t)f * H * W1 * D;
     int16_t* row = Cf + (size_t)y * W1 * D;
     for (int d = threadIdx.x; d < D; d += blockDim.x) row[d] = e.fullDP ? (int16_t)e.P2 : Cf[d];
+    if (Rv) {
+        uint8_t* Rf = Rv + (size_t)f * H * W1 * (D / 2);
+        uint8_t* rrow = Rf + (size_t)y * W1 * (D / 2);
+        for (int k = threadIdx.x; k < D / 2; k += blockDim.x)
+            rrow[k] = e.fullDP ? (uint8_t)(e.P2 * 0x11) : Rf[k];
+    }
 }
 
 // Rows ybot .. H - 1, all columns (grid: 8-element chunks x rows x frames):
 // row ylast (column 0: C(0, 0, d) unless FIRSTCOL_FIX) or P2 (MODE_HH).  D is a
 // multiple of 16, so a 16-byte chunk never straddles two columns.
 __global__ __launch_bounds__(256) void sgbm_cost_fixup_bottom_kernel(int16_t* __restrict__ C, int H,
-                                                                     SgbmEff e, int ylast, int ybot)
+                                                                     SgbmEff e, int ylast, int ybot,
+                                                                     uint8_t* __restrict__ Rv)
 {
     const int D = e.D, W1 = e.W1;
     const size_t chunk = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // 8 elements each
@@ -598,15 +675,20 @@ __global__ __launch_bounds__(256) void sgbm_cost_fixup_bottom_kernel(int16_t* __
     int16_t* Cf = C + (size_t)f * H * rowlen;
     uint4* dst = (uint4*)(Cf + (size_t)y * rowlen) + chunk;
     uint4 v;
+    const bool fix = (e.variant & MVSV_VARIANT_FIRSTCOL_FIX) != 0;
+    const bool col0 = chunk * 8 < (size_t)D && !fix;
     if (e.fullDP) {
         const uint32_t p2 = (uint32_t)(e.P2 & 0xffff) * 0x10001u;
         v = make_uint4(p2, p2, p2, p2);
     } else {
-        const bool fix = (e.variant & MVSV_VARIANT_FIRSTCOL_FIX) != 0;
-        const bool col0 = chunk * 8 < (size_t)D && !fix;
         v = *((const uint4*)(Cf + (col0 ? 0 : (size_t)ylast * rowlen)) + chunk);
     }
     *dst = v;
+    if (Rv) {  // the chunk's 8 residual nibbles: one dword
+        uint32_t* Rf = (uint32_t*)(Rv + (size_t)f * H * (rowlen / 2));
+        Rf[(size_t)y * (rowlen / 8) + chunk] =
+            e.fullDP ? (uint32_t)e.P2 * 0x11111111u : Rf[(col0 ? 0 : (size_t)ylast * (rowlen / 8)) + chunk];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -738,6 +820,62 @@ struct Vec<8> {
     {
         *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
         *(uint4*)(p + 8) = make_uint4(v[4], v[5], v[6], v[7]);
+    }
+};
+
+// Cost input of the direction passes: the int16 cost volume C (RES = false)
+// or the residual plane R (RES = true, two nibbles per byte, see above).
+// Offsets are in cost elements (disparity units) either way; get() returns the
+// lane's NP packed (d, d+1) u16 pairs.
+template <int NP, bool RES>
+struct CostIn;
+template <int NP>
+struct CostIn<NP, false> {
+    Vec<NP> b;
+    static __device__ __forceinline__ const void* at(const void* base, ptrdiff_t e)
+    {
+        return (const int16_t*)base + e;
+    }
+    __device__ __forceinline__ void load(const void* p) { b.load((const int16_t*)p); }
+    __device__ __forceinline__ void get(uint32_t (&c)[NP]) const
+    {
+#pragma unroll
+        for (int i = 0; i < NP; i++) c[i] = b.v[i];
+    }
+};
+template <int NP>
+struct CostIn<NP, true> {
+    static constexpr int NWD = NP >= 8 ? 2 : 1;
+    uint32_t w[NWD];
+    static __device__ __forceinline__ const void* at(const void* base, ptrdiff_t e)
+    {
+        return (const uint8_t*)base + e / 2;  // e is even (D and the lane offsets are)
+    }
+    __device__ __forceinline__ void load(const void* p)
+    {
+        if constexpr (NP == 1) {
+            w[0] = *(const uint8_t*)p;
+        } else if constexpr (NP == 2) {
+            w[0] = *(const uint16_t*)p;
+        } else if constexpr (NP == 4) {
+            w[0] = *(const uint32_t*)p;
+        } else {
+            const uint2 t = *(const uint2*)p;
+            w[0] = t.x;
+            w[1] = t.y;
+        }
+    }
+    // byte k = (R(2k), R(2k+1)) nibbles -> pair k = R(2k) | R(2k+1) << 16:
+    // low nibbles E and high nibbles O as bytes, then one v_perm_b32 per pair
+    __device__ __forceinline__ void get(uint32_t (&c)[NP]) const
+    {
+#pragma unroll
+        for (int q = 0; q < NWD; q++) {
+            const uint32_t E = w[q] & 0x0f0f0f0fu, O = (w[q] >> 4) & 0x0f0f0f0fu;
+#pragma unroll
+            for (int k = 0; k < (NP < 4 ? NP : 4); k++)
+                c[4 * q + k] = __builtin_amdgcn_perm(O, E, 0x0c000c00u | (uint32_t)k | ((uint32_t)(4 + k) << 16));
+        }
     }
 };
 
@@ -1133,24 +1271,15 @@ __device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t b, uint32_t 
                                             __builtin_bit_cast(u16x2, c));
 }
 
-// Two independent u16 minima over each 16-lane row (packed in one dword).
-__device__ __forceinline__ uint32_t row_min_u16x2(uint32_t v)
-{
-    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false));
-    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false));
-    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false));
-    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, false));
-    return v;
-}
-
 constexpr int kPath16PF = 12;
 
-template <int NP, bool FIRST, typename AccT, bool NW = false>
-__device__ __forceinline__ void path16_lines(const int16_t* __restrict__ C, AccT* __restrict__ A,
+template <int NP, bool FIRST, typename AccT, bool NW = false, bool RES = false>
+__device__ __forceinline__ void path16_lines(const void* __restrict__ C, AccT* __restrict__ A,
                                              AccT* __restrict__ dummy, int H, int W1, int D, int dx,
                                              int dy, int P1, int P2, int bx, int f)
 {
     using AV = AccVec<NP, AccT>;
+    using CI = CostIn<NP, RES>;
     constexpr int PF = kPath16PF;
     const int lane = threadIdx.x & 63;
     const int row = lane >> 4, rl = lane & 15;
@@ -1166,7 +1295,7 @@ __device__ __forceinline__ void path16_lines(const int16_t* __restrict__ C, AccT
     const ptrdiff_t step = ((ptrdiff_t)dy * W1 + dx) * D;
     const int d0 = rl * 2 * NP;
     const size_t off = f * frame + ((size_t)g.ys * W1 + g.xs) * D + d0;
-    const int16_t* cp = C + off;
+    const void* cp = CI::at(C, (ptrdiff_t)off);
     AccT* ap = acc_add(A, (ptrdiff_t)off);
     AccT* dp = acc_add(dummy, (ptrdiff_t)threadIdx.x * 2 * NP);
     const int last = max(len - 1, 0);
@@ -1177,19 +1306,18 @@ __device__ __forceinline__ void path16_lines(const int16_t* __restrict__ C, AccT
     const uint32_t p2x2 = (uint32_t)(P2 & 0xffff) * 0x10001u;
     int minp = 0;
 
-    Vec<NP> cb[PF];
+    CI cb[PF];
     uint32_t ab[PF][NP];
 #pragma unroll
     for (int j = 0; j < PF; j++) {
         const ptrdiff_t t = min(j, last);
-        cb[j].load(cp + t * step);
+        cb[j].load(CI::at(cp, t * step));
         if constexpr (!FIRST) AV::load(acc_add(ap, t * step), ab[j]);
     }
     auto body = [&](int s, int j) {
         const uint32_t delta2 = sgm_delta2<NW>(minp, P2);
         uint32_t c[NP], ln[NP], o[NP], tt[NP];
-#pragma unroll
-        for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
+        cb[j].get(c);
         sgm_step_row_t<NP, NW>(lp, delta2, p1x2, c, ln, tt);
         minp = row_min_i32(lane_min_row<NP>(ln));
 #pragma unroll
@@ -1210,7 +1338,7 @@ __device__ __forceinline__ void path16_lines(const int16_t* __restrict__ C, AccT
         for (int j = 0; j < PF; j++) {
             body(s + j, j);
             const ptrdiff_t t = min(s + j + PF, last);
-            cb[j].load(cp + t * step);
+            cb[j].load(CI::at(cp, t * step));
             if constexpr (!FIRST) AV::load(acc_add(ap, t * step), ab[j]);
         }
     }
@@ -1221,13 +1349,13 @@ __device__ __forceinline__ void path16_lines(const int16_t* __restrict__ C, AccT
 }
 
 
-template <int NP, bool FIRST, typename AccT, bool NW = false>
-__global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restrict__ C,
+template <int NP, bool FIRST, typename AccT, bool NW = false, bool RES = false>
+__global__ __launch_bounds__(256) void sgbm_path16_kernel(const void* __restrict__ C,
                                                           AccT* __restrict__ A,
                                                           AccT* __restrict__ dummy, int H, int W1,
                                                           int D, int dx, int dy, int P1, int P2)
 {
-    path16_lines<NP, FIRST, AccT, NW>(C, A, dummy, H, W1, D, dx, dy, P1, P2, blockIdx.x, blockIdx.y);
+    path16_lines<NP, FIRST, AccT, NW, RES>(C, A, dummy, H, W1, D, dx, dy, P1, P2, blockIdx.x, blockIdx.y);
 }
 
 // All directions of a small launch at once (blockIdx.z = direction k, its
@@ -1237,15 +1365,15 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const int16_t* __restr
 struct PathDirs {
     int dx[7], dy[7];
 };
-template <int NP, typename AccT, bool NW>
-__global__ __launch_bounds__(256) void sgbm_pathdirs16_kernel(const int16_t* __restrict__ C,
+template <int NP, typename AccT, bool NW, bool RES = false>
+__global__ __launch_bounds__(256) void sgbm_pathdirs16_kernel(const void* __restrict__ C,
                                                               AccT* __restrict__ A, size_t plane,
                                                               AccT* __restrict__ dummy, int H, int W1,
                                                               int D, PathDirs dirs, int P1, int P2)
 {
     const int k = blockIdx.z;
-    path16_lines<NP, true, AccT, NW>(C, acc_add(A, (ptrdiff_t)k * (ptrdiff_t)plane), dummy, H, W1, D,
-                                     dirs.dx[k], dirs.dy[k], P1, P2, blockIdx.x, blockIdx.y);
+    path16_lines<NP, true, AccT, NW, RES>(C, acc_add(A, (ptrdiff_t)k * (ptrdiff_t)plane), dummy, H, W1, D,
+                                          dirs.dx[k], dirs.dy[k], P1, P2, blockIdx.x, blockIdx.y);
 }
 
 // ---------------------------------------------------------------------------
@@ -1372,15 +1500,16 @@ __device__ __forceinline__ size_t tri_slot(int chain, int k, int t, int nchains,
     return ((((size_t)k * nchains + chain) * H + t) * 4) * LPC * TriGran<NP>::NG;
 }
 
-template <int NP, int WV, int LPC, typename AccT, bool NW = false>
+template <int NP, int WV, int LPC, typename AccT, bool NW = false, bool RES = false>
 __global__ __launch_bounds__((TriCfg<NP, WV, LPC>::kThreads))
 __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm_tri_kernel(
-    const int16_t* __restrict__ C, AccT* __restrict__ A, size_t plane, AccT* __restrict__ dummy,
+    const void* __restrict__ C, AccT* __restrict__ A, size_t plane, AccT* __restrict__ dummy,
     int H, int W1, int D, int npass, int P1, int P2, unsigned long long* __restrict__ bnd,
     unsigned epoch, int nframes, int nstrips, int* __restrict__ status, unsigned spin_limit,
     int* __restrict__ report, unsigned long long* __restrict__ stats, int trace_h, long long ticket0)
 {
     using AV = AccVec<NP, AccT>;
+    using CI = CostIn<NP, RES>;
     using TL = TriLayout<NP, WV, LPC>;
     using TG = TriGran<NP>;
     constexpr int NG = TG::NG;
@@ -1438,7 +1567,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
     unsigned long long st_t0 = stats ? __builtin_amdgcn_s_memtime() : 0ull, st_spin = 0, st_n = 0;
     const int d0 = rl * 2 * NP;
     const size_t frame = (size_t)H * W1 * D;
-    const int16_t* Cf = C + f * frame + d0;
+    const void* Cf = CI::at(C, (ptrdiff_t)(f * frame + d0));
     AccT* Af = acc_add(A, (ptrdiff_t)(f * frame + d0));
     AccT* dp = acc_add(dummy, (ptrdiff_t)threadIdx.x * 2 * NP);
     const uint32_t p1x2 = (uint32_t)(P1 & 0xffff) * 0x10001u;
@@ -1558,7 +1687,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
 #pragma unroll
     for (int p = 0; p < NP; p++) la[p] = 0u;
     int ma = 0;
-    Vec<NP> cb[PF];
+    CI cb[PF];
     unsigned long long bg[BF][NG];
 
     __syncthreads();  // LDS zeroed
@@ -1570,7 +1699,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
         for (int j = 0; j < BF; j++) bload(tb + j, bg[j]);
     } else {
 #pragma unroll
-        for (int j = 0; j < PF; j++) cb[j].load(Cf + cell_off(min(tb + j, te - 1)));
+        for (int j = 0; j < PF; j++) cb[j].load(CI::at(Cf, cell_off(min(tb + j, te - 1))));
     }
     __syncthreads();
 
@@ -1600,9 +1729,8 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm
         const bool valid = x >= 0 && x < W1;
         const bool allv = __all(valid);
         uint32_t c[NP];
-#pragma unroll
-        for (int p = 0; p < NP; p++) c[p] = cb[j % PF].v[p];
-        cb[j % PF].load(Cf + cell_off(min(t + PF, te - 1)));
+        cb[j % PF].get(c);
+        cb[j % PF].load(CI::at(Cf, cell_off(min(t + PF, te - 1))));
         // the column minimum of one direction (packed (m, m) in the no-wrap
         // form) and the next step's delta from it
         auto dmin = [&](const uint32_t (&n)[NP]) -> int {
@@ -2404,6 +2532,16 @@ static bool sgbm_no_wrap(const SgbmEff& e)
     return (long)e.P2 + bs * bs * (2L * e.ftzero + 63) + e.P2 <= 32767;
 }
 
+// The direction passes read the residual plane (see its definition above)
+// when it is exact and smaller: no-wrap regime, residuals <= 3 * P2 in a
+// nibble, a 16-lane path schedule (1 = strips + lines, 2 = side by side) and
+// D <= 128 (one cost kernel wave segment holds a pixel's D costs).
+static bool use_residual(const mvsv_ctx* ctx, const SgbmEff& e, int sched)
+{
+    return ctx->cost_res && (sched == 1 || sched == 2) && sgbm_no_wrap(e) && 3 * e.P2 <= 15 &&
+           (e.D == 32 || e.D == 64 || e.D == 128);
+}
+
 static bool use_strips(const mvsv_ctx* ctx, const SgbmEff& e, int H)
 {
     return ctx->tri && (size_t)H * e.W1 * e.D < ((size_t)1 << 31);
@@ -2430,8 +2568,8 @@ static int path_schedule(const mvsv_ctx* ctx, const SgbmEff& e, int H, int n)
     return use_strips(ctx, e, H) ? 1 : 0;
 }
 
-template <int NP, int WV, int LPC, typename AccT, bool NW>
-int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
+template <int NP, int WV, int LPC, typename AccT, bool NW, bool RES>
+int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const void* Cv, AccT* Av, size_t plane,
                   int npass)
 {
     using TL = TriLayout<NP, WV, LPC>;
@@ -2475,18 +2613,18 @@ int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, Ac
         (void)hipMalloc(&stats, (size_t)grid.x * sb * 8);
         (void)hipMemset(stats, 0, (size_t)grid.x * sb * 8);
     }
-    // Tickets only where some block could wait for a CU: a launch of at most
-    // one block per CU is resident all at once, whatever the dispatch order
-    // (and there blockIdx order keeps strips that share a CU far apart in the
-    // chain -- one early, one late -- instead of neighbours running at the
-    // same time: config 5, two frames, 2.87 vs 3.61 ms).
-    const bool tickets = ctx->strip_tickets && (int)grid.x > ctx->cus;
+    // Strip tickets for every launch (round 4): a launch of at most one block
+    // per CU is not resident all at once when other work shares the GPU
+    // (stream lanes, batches in flight), so blockIdx order would rest on
+    // in-order dispatch; tickets never do.  MVSV_OPT_STRIP_TICKETS = 0 keeps
+    // blockIdx order for A/B runs.
+    const bool tickets = ctx->strip_tickets != 0;
     if (TL::kBytes > 65536 &&
-        (rc = check_hip(ctx, hipFuncSetAttribute((const void*)sgbm_tri_kernel<NP, WV, LPC, AccT, NW>,
+        (rc = check_hip(ctx, hipFuncSetAttribute((const void*)sgbm_tri_kernel<NP, WV, LPC, AccT, NW, RES>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)TL::kBytes),
                         "sgbm strip LDS attribute")))
         return rc;
-    hipLaunchKernelGGL((sgbm_tri_kernel<NP, WV, LPC, AccT, NW>), grid, dim3(TriCfg<NP, WV, LPC>::kThreads), TL::kBytes,
+    hipLaunchKernelGGL((sgbm_tri_kernel<NP, WV, LPC, AccT, NW, RES>), grid, dim3(TriCfg<NP, WV, LPC>::kThreads), TL::kBytes,
                        ctx->stream, Cv, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, npass, e.P1,
                        e.P2, (unsigned long long*)ctx->tri_bnd.ptr, epoch, n, nstrips,
                        (int*)ctx->status.ptr, ctx->spin_limit, ctx->report_target, stats, trace_h,
@@ -2540,8 +2678,10 @@ int launch_tri_wv(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, Ac
 // over more CUs at about half the per-step work (640x480, one frame: strips
 // 0.62 -> 0.41 ms; 4 waves per strip: 0.42 ms, its longer chain of strips
 // eats the shorter steps).  MVSV_OPT_STRIP_WAVES forces either shape.
-template <int NP, int LPC, typename AccT, bool NW>
-int launch_tri_lpc(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
+// (Round 3's 8-lanes-per-column variant, LPC = 8, measured slower and is no
+// longer instantiated; the kernel keeps the LPC parameter.)
+template <int NP, int LPC, typename AccT, bool NW, bool RES>
+int launch_tri_lpc(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const void* Cv, AccT* Av, size_t plane,
                    int npass)
 {
     constexpr int wide = tri_wide_waves<NP, LPC>(), narrow = tri_narrow_waves<NP, LPC>();
@@ -2551,30 +2691,26 @@ int launch_tri_lpc(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, A
         const long long blocks = (long long)npass * n * ((e.W1 + H - 1 + cpw * wide - 1) / (cpw * wide));
         wv = blocks < ctx->cus ? narrow : wide;
     }
-    if (wv == narrow) return launch_tri_wv<NP, narrow, LPC, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass);
-    return launch_tri_wv<NP, wide, LPC, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass);
+    if (wv == narrow) return launch_tri_wv<NP, narrow, LPC, AccT, NW, RES>(ctx, n, H, e, Cv, Av, plane, npass);
+    return launch_tri_wv<NP, wide, LPC, AccT, NW, RES>(ctx, n, H, e, Cv, Av, plane, npass);
 }
 
-// D = 128 (NP = 4 at 16 lanes per column) may run on 8 lanes per column with
-// 16 disparities per lane (ctx->strip_lpc, MVSV_STRIP_LPC); every other D keeps
-// 16 lanes.  The planes and the cost volume do not depend on the choice.
-template <int NP, typename AccT, bool NW>
-int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, AccT* Av, size_t plane,
+template <int NP, typename AccT, bool NW, bool RES>
+int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const void* Cv, AccT* Av, size_t plane,
                int npass)
 {
-    if constexpr (NP == 4) {
-        if (ctx->strip_lpc == 8) return launch_tri_lpc<8, 8, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass);
-    }
-    return launch_tri_lpc<NP, 16, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass);
+    return launch_tri_lpc<NP, 16, AccT, NW, RES>(ctx, n, H, e, Cv, Av, plane, npass);
 }
 
 // Sheared-strip schedule: the down pass ((1,1) (0,1) (-1,1)), the up pass
 // ((1,-1) (0,-1) (-1,-1), MODE_HH) and the L->R lines each write their own
 // accumulator plane; the L->R lines run on a second stream beside the strip
-// kernel, and the final kernel (R->L + WTA) sums the planes.
-template <int NP, typename AccT, bool NW>
-int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, AccT* Av,
-                     size_t plane, int16_t* raw)
+// kernel, and the final kernel (R->L + WTA) sums the planes.  The direction
+// passes read Cin -- the cost volume, or (RES) its residual plane -- and the
+// final kernel the cost volume Cv.
+template <int NP, typename AccT, bool NW, bool RES = false>
+int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, const void* Cin,
+                     AccT* Av, size_t plane, int16_t* raw)
 {
     hipStream_t s = ctx->stream;
     int rc;
@@ -2606,7 +2742,7 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
         auto lines = [&]() {
             StageTimer tl(ctx, kStageLines, ls);
             dim3 grid((num_lines(1, 0, e.W1, H) + 15) / 16, n);
-            hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT, NW>), grid, dim3(256), 0, ls, Cv,
+            hipLaunchKernelGGL((sgbm_path16_kernel<NP, true, AccT, NW, RES>), grid, dim3(256), 0, ls, Cin,
                                acc_add(Av, (ptrdiff_t)npass * (ptrdiff_t)plane), dummy, H, e.W1,
                                e.D, 1, 0, e.P1, e.P2);
         };
@@ -2616,7 +2752,7 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
         if ((rc = check_hip(ctx, hipGetLastError(), "sgbm L->R lines"))) return rc;
         {
             StageTimer ts(ctx, kStageStrips);
-            if ((rc = launch_tri<NP, AccT, NW>(ctx, n, H, e, Cv, Av, plane, npass))) return rc;
+            if ((rc = launch_tri<NP, AccT, NW, RES>(ctx, n, H, e, Cin, Av, plane, npass))) return rc;
         }
         if (aux_mode != 1) lines();
         if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_join, ctx->aux), "join")) ||
@@ -2643,7 +2779,7 @@ int launch_paths16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t
     if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
     AccT* dummy = (AccT*)ctx->dummy.ptr;
     const size_t plane = (size_t)n * H * e.W1 * e.D;
-    if (use_strips(ctx, e, H)) return launch_paths_tri<NP, AccT, false>(ctx, n, H, W, e, Cv, Av, plane, raw);
+    if (use_strips(ctx, e, H)) return launch_paths_tri<NP, AccT, false>(ctx, n, H, W, e, Cv, Cv, Av, plane, raw);
     const int ndir = e.fullDP ? 7 : 4;
     for (int k = 0; k < ndir; k++) {
         int dx = e.fullDP ? dirs_hh[k][0] : dirs_sgbm[k][0];
@@ -2702,9 +2838,9 @@ int launch_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* 
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels");
 }
 
-template <int NP, typename AccT, bool NW>
-int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, AccT* Av,
-                      int16_t* raw)
+template <int NP, typename AccT, bool NW, bool RES = false>
+int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, const void* Cin,
+                      AccT* Av, int16_t* raw)
 {
     static const int dirs_sgbm[4][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}};
     static const int dirs_hh[7][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}, {1, -1}, {0, -1}, {-1, -1}};
@@ -2719,8 +2855,8 @@ int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int1
     const size_t plane = (size_t)n * H * e.W1 * e.D;
     {
         StageTimer tm(ctx, kStagePath);
-        hipLaunchKernelGGL((sgbm_pathdirs16_kernel<NP, AccT, NW>), dim3((maxnl + 15) / 16, n, ndir), dim3(256),
-                           0, ctx->stream, Cv, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, pd, e.P1,
+        hipLaunchKernelGGL((sgbm_pathdirs16_kernel<NP, AccT, NW, RES>), dim3((maxnl + 15) / 16, n, ndir), dim3(256),
+                           0, ctx->stream, Cin, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, pd, e.P1,
                            e.P2);
     }
     StageTimer tm(ctx, kStageFinal);
@@ -2731,9 +2867,11 @@ int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int1
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels (directions side by side)");
 }
 
+// Rv: the residual plane written by the cost kernel (nullptr: none; only ever
+// set in the no-wrap regime with 3 * P2 <= 15, use_residual)
 template <int NP>
 int launch_paths16_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv,
-                       void* Av, int16_t* raw)
+                       const uint8_t* Rv, void* Av, int16_t* raw)
 {
     if (path_schedule(ctx, e, H, n) == 2) {
         int rc;
@@ -2742,21 +2880,28 @@ int launch_paths16_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int
         // one plane per direction: a delta <= P2 in a nibble (4 or 7 of them <= 105
     // per byte lane), a byte (when all directions' sum fits) or a u16
         if (e.P2 <= 15) {
-            if (sgbm_no_wrap(e)) return launch_paths_dirs<NP, nib2_t, true>(ctx, n, H, W, e, Cv, (nib2_t*)Av, raw);
-            return launch_paths_dirs<NP, nib2_t, false>(ctx, n, H, W, e, Cv, (nib2_t*)Av, raw);
+            if (sgbm_no_wrap(e)) {
+                if constexpr (NP <= 4)
+                    if (Rv) return launch_paths_dirs<NP, nib2_t, true, true>(ctx, n, H, W, e, Cv, Rv, (nib2_t*)Av, raw);
+                return launch_paths_dirs<NP, nib2_t, true>(ctx, n, H, W, e, Cv, Cv, (nib2_t*)Av, raw);
+            }
+            return launch_paths_dirs<NP, nib2_t, false>(ctx, n, H, W, e, Cv, Cv, (nib2_t*)Av, raw);
         }
         // the final kernel sums the planes in the plane's element type
-        if (acc_is_u8(e)) return launch_paths_dirs<NP, uint8_t, false>(ctx, n, H, W, e, Cv, (uint8_t*)Av, raw);
-        return launch_paths_dirs<NP, uint16_t, false>(ctx, n, H, W, e, Cv, (uint16_t*)Av, raw);
+        if (acc_is_u8(e)) return launch_paths_dirs<NP, uint8_t, false>(ctx, n, H, W, e, Cv, Cv, (uint8_t*)Av, raw);
+        return launch_paths_dirs<NP, uint16_t, false>(ctx, n, H, W, e, Cv, Cv, (uint16_t*)Av, raw);
     }
     if (use_strips(ctx, e, H) && acc_is_nib(e)) {
         int rc;
         if ((rc = ensure(ctx, ctx->dummy, 512 * 16 * 2 * NP, "sgbm dummy slots"))) return rc;
         if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
         const size_t plane = (size_t)n * H * e.W1 * e.D;
-        if (sgbm_no_wrap(e))
-            return launch_paths_tri<NP, nib2_t, true>(ctx, n, H, W, e, Cv, (nib2_t*)Av, plane, raw);
-        return launch_paths_tri<NP, nib2_t, false>(ctx, n, H, W, e, Cv, (nib2_t*)Av, plane, raw);
+        if (sgbm_no_wrap(e)) {
+            if constexpr (NP <= 4)
+                if (Rv) return launch_paths_tri<NP, nib2_t, true, true>(ctx, n, H, W, e, Cv, Rv, (nib2_t*)Av, plane, raw);
+            return launch_paths_tri<NP, nib2_t, true>(ctx, n, H, W, e, Cv, Cv, (nib2_t*)Av, plane, raw);
+        }
+        return launch_paths_tri<NP, nib2_t, false>(ctx, n, H, W, e, Cv, Cv, (nib2_t*)Av, plane, raw);
     }
     if (acc_is_u8(e)) return launch_paths16<NP, uint8_t>(ctx, n, H, W, e, Cv, (uint8_t*)Av, raw);
     return launch_paths16<NP, uint16_t>(ctx, n, H, W, e, Cv, (uint16_t*)Av, raw);
@@ -2772,7 +2917,7 @@ int launch_paths_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
 
 }  // namespace
 
-using Cost2Kern = void (*)(const uint64_t*, int, int, SgbmEff, int, int16_t*);
+using Cost2Kern = void (*)(const uint64_t*, int, int, SgbmEff, int, int16_t*, uint8_t*);
 template <int STG, int PPC>
 static Cost2Kern cost2_pick_nr(int nr)
 {
@@ -2797,9 +2942,11 @@ static Cost2Kern cost2_pick(int nr, int stg, int ppc)
 }
 
 // Cost-volume launch: the register-ring kernel when blockSize <= 15 and the
-// tile fits, else the LDS-ring kernel.
+// tile fits, else the LDS-ring kernel.  *Rv (residual plane, may be nullptr)
+// is written by the register-ring kernel only: the LDS-ring fallback sets it
+// to nullptr, and the direction passes then read C.
 static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int TY,
-                       const uint64_t* pre, int16_t* Cv, bool* pinned_hh)
+                       const uint64_t* pre, int16_t* Cv, uint8_t** Rv, bool* pinned_hh)
 {
     *pinned_hh = false;
     hipStream_t s = ctx->stream;
@@ -2825,12 +2972,13 @@ static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int
             {
                 StageTimer tm(ctx, kStageCost);
                 hipLaunchKernelGGL(kern, grid2, dim3(kCost2Threads), l2.bytes, s, pre, W, H, e, TY,
-                                   Cv);
+                                   Cv, *Rv);
             }
             *pinned_hh = e.fullDP != 0;  // MODE_HH fix-up rows/column written by the kernel
             return check_hip(ctx, hipGetLastError(), "sgbm cost kernel");
         }
     }
+    *Rv = nullptr;
     CostLayout lay = cost_layout(e.D, e.SW2, e.SH2, TY);
     if (lay.nLmax + lay.nRmax + 1 > 256 * kStageRegs)
         return set_error(ctx, MVSV_E_INVALID_ARG, "numDisparities too large for the GPU cost kernel");
@@ -2878,6 +3026,12 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
                      "sgbm path-delta accumulator")))
         return rc;
     if ((rc = ensure(ctx, ctx->raw, (size_t)n * plane * 2, "sgbm raw disparity"))) return rc;
+    // residual plane for the direction passes (0.5 byte per cost instead of 2)
+    uint8_t* Rv = nullptr;
+    if (use_residual(ctx, e, sched)) {
+        if ((rc = ensure(ctx, ctx->cres, (size_t)n * vol / 2, "sgbm cost residual plane"))) return rc;
+        Rv = (uint8_t*)ctx->cres.ptr;
+    }
     uint64_t* pre = (uint64_t*)ctx->pre.ptr;
     int16_t* Cv = (int16_t*)ctx->cost.ptr;
     void* Sv = ctx->agg.ptr;
@@ -2919,7 +3073,7 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
         }
     }
     bool pinned_hh = false;
-    if ((rc = launch_cost(ctx, n, W, H, e, TY, pre, Cv, &pinned_hh))) return rc;
+    if ((rc = launch_cost(ctx, n, W, H, e, TY, pre, Cv, &Rv, &pinned_hh))) return rc;
 
     const int ybot = std::max(H - e.SH2, 1);     // first row that is never recomputed
     const int ylast = std::max(H - e.SH2 - 1, 0);  // last recomputed row
@@ -2931,11 +3085,11 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
         // bottom kernel (the rows are disjoint).
         const bool fix = (e.variant & MVSV_VARIANT_FIRSTCOL_FIX) != 0;
         if (ybot > 1 && !fix)
-            hipLaunchKernelGGL(sgbm_cost_fixup_col0_kernel, dim3(ybot - 1, n), dim3(256), 0, s, Cv, H, e);
+            hipLaunchKernelGGL(sgbm_cost_fixup_col0_kernel, dim3(ybot - 1, n), dim3(256), 0, s, Cv, H, e, Rv);
         if (ybot < H) {
             const size_t chunks = ((size_t)e.W1 * e.D + 7) / 8;
             hipLaunchKernelGGL(sgbm_cost_fixup_bottom_kernel, dim3((unsigned)((chunks + 255) / 256), H - ybot, n),
-                               dim3(256), 0, s, Cv, H, e, ylast, ybot);
+                               dim3(256), 0, s, Cv, H, e, ylast, ybot, Rv);
         }
         if ((rc = check_hip(ctx, hipGetLastError(), "sgbm cost fixup"))) return rc;
     }
@@ -2944,10 +3098,10 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     const bool wide = ctx->path16 && (e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256);
     if (wide) {
         switch (e.D) {
-        case 32: rc = launch_paths16_acc<1>(ctx, n, H, W, e, Cv, Sv, raw); break;
-        case 64: rc = launch_paths16_acc<2>(ctx, n, H, W, e, Cv, Sv, raw); break;
-        case 128: rc = launch_paths16_acc<4>(ctx, n, H, W, e, Cv, Sv, raw); break;
-        default: rc = launch_paths16_acc<8>(ctx, n, H, W, e, Cv, Sv, raw); break;
+        case 32: rc = launch_paths16_acc<1>(ctx, n, H, W, e, Cv, Rv, Sv, raw); break;
+        case 64: rc = launch_paths16_acc<2>(ctx, n, H, W, e, Cv, Rv, Sv, raw); break;
+        case 128: rc = launch_paths16_acc<4>(ctx, n, H, W, e, Cv, Rv, Sv, raw); break;
+        default: rc = launch_paths16_acc<8>(ctx, n, H, W, e, Cv, nullptr, Sv, raw); break;
         }
     } else if (np == 1) rc = launch_paths_acc<1>(ctx, n, H, W, e, Cv, Sv, raw);
     else if (np == 2) rc = launch_paths_acc<2>(ctx, n, H, W, e, Cv, Sv, raw);

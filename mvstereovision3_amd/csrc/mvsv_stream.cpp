@@ -221,7 +221,7 @@ static void copy_options(mvsv_ctx* d, const mvsv_ctx* s)
     d->tri = s->tri;
     d->path_sched = s->path_sched;
     d->strip_waves = s->strip_waves;
-    d->strip_lpc = s->strip_lpc;
+    d->cost_res = s->cost_res;
     d->lines_aux = s->lines_aux;
     d->strip_tickets = s->strip_tickets;
     d->bm2 = s->bm2;

@@ -107,3 +107,28 @@ def test_strip_order_batch_device(gpu, mvsv, oracle, tickets):
         want = oracle.sgbm(L, R, p)
         for got in outs:
             assert np.array_equal(got[i], want), f"tickets={tickets} frame {i}: " + report(got[i], want)
+
+
+@pytest.mark.parametrize("tickets", [1, 0])
+def test_strip_order_one_frame_resident(gpu, mvsv, oracle, tickets):
+    """A one-frame strip launch (fewer blocks than CUs: narrow strips, all
+    resident at once on an idle GPU) by ticket -- the default for every launch
+    size since round 4 -- and by blockIdx, twice in a row; bit-exact."""
+    from mvstereovision3_amd import _lib
+    rng = np.random.default_rng(9350)
+    H, W, D = 200, 520, 128
+    L, R = rand_pair(rng, H, W, 30, 0)
+    kw = dict(minDisparity=1, numDisparities=D, blockSize=13, P1=2, P2=5, disp12MaxDiff=1,
+              uniquenessRatio=0, speckleWindowSize=0, speckleRange=2, mode=1)
+    gots = []
+    try:
+        _lib.set_option(_lib.OPT_PATH_SCHEDULE, 1)
+        _lib.set_option(_lib.OPT_STRIP_TICKETS, tickets)
+        for _ in range(2):
+            got, want = sgbm_both(mvsv, oracle, L, R, **kw)
+            gots.append(got)
+    finally:
+        _lib.set_option(_lib.OPT_STRIP_TICKETS, 1)
+        _lib.set_option(_lib.OPT_PATH_SCHEDULE, 0)
+    for got in gots:
+        assert np.array_equal(got, want), f"tickets={tickets}: " + report(got, want)
