@@ -70,7 +70,16 @@ class InflightBatches:
     frame-parallel batch mode; every step still computes its whole batch).
     ``compute(L, R, out)`` is called inside the slot's stream and context; the
     gather (world > 1 or ``collective``) follows it on the same stream, in step
-    order on every rank."""
+    order on every rank.
+
+    Synchronisation contract: step() makes the slot wait for the caller's
+    current stream (inputs written there are ready), but the caller's stream
+    does NOT wait for the slot.  Before reading ``last_out`` / ``gathered`` or
+    writing new data into ``left`` / ``right`` on the caller's stream, call
+    join() (or synchronize the device); the input and output tensors are
+    recorded on the slot streams, so dropping the last reference to one of
+    them never hands its memory to another allocation while a slot still uses
+    it."""
 
     def __init__(self, left, right, make_out, compute: Callable, n: int, device, rank: int = 0,
                  world: int = 1, gather: bool = True, dst: int = 0, collective: bool = False):
@@ -91,6 +100,8 @@ class InflightBatches:
         stream, ctx, out = self.slots[self.k % len(self.slots)]
         self.k += 1
         stream.wait_stream(torch.cuda.current_stream(stream.device))  # inputs ready
+        for t in (self.left, self.right, out):
+            t.record_stream(stream)  # the allocator keeps them alive for this slot
         with torch.cuda.stream(stream), use_context(ctx):
             self.compute(self.left, self.right, out)
             if self.gather:
@@ -102,7 +113,8 @@ class InflightBatches:
         return [c for _, c, _ in self.slots]
 
     def join(self):
-        """Make the caller's current stream wait for every slot."""
+        """Make the caller's current stream wait for every slot: required before
+        reading a step's results or refilling the inputs on that stream."""
         import torch
         cur = torch.cuda.current_stream(self.slots[0][0].device)
         for s, _, _ in self.slots:

@@ -526,6 +526,10 @@ static int host_call(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* 
     if (rc) return set_error(ctx, rc, why);
     if (sgbm && (rc = check_report(ctx))) return rc;  // an earlier device call's give-up
     DeviceGuard dev_guard(ctx->device);
+    // every exit after the first enqueue records the context's last-use event,
+    // so a later stream switch waits for whatever this call left queued
+    return mark_last_use(ctx, [&]() -> int {
+    int rc;
     size_t fb = (size_t)W * H;
     if ((rc = ensure(ctx, ctx->h_left, fb, "left staging"))) return rc;
     if ((rc = ensure(ctx, ctx->h_right, fb, "right staging"))) return rc;
@@ -544,6 +548,7 @@ static int host_call(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* 
     // only an SGBM call reads the sticky give-up word: a BM call's valid map is
     // returned and the word waits for the next SGBM call or mvsv_synchronize
     return sgbm ? check_report(ctx) : MVSV_OK;
+    }());
 }
 
 int mvsv_sgbm(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t* R, size_t rs, int W,
@@ -580,6 +585,7 @@ int mvsv_dmap2pcl(mvsv_ctx* ctx, const char* path, const int16_t* dmap, size_t s
     if (!path || !dmap || !Q || W <= 0 || H <= 0 || st < (size_t)W)
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad dmap2pcl arguments");
     DeviceGuard dev_guard(ctx->device);
+    return mark_last_use(ctx, [&]() -> int {
     const size_t px = (size_t)W * H;
     int rc;
     if ((rc = ensure(ctx, ctx->h_out, px * 2, "dmap staging"))) return rc;
@@ -609,6 +615,7 @@ int mvsv_dmap2pcl(mvsv_ctx* ctx, const char* path, const int16_t* dmap, size_t s
     if (rc == MVSV_E_IO) return set_error(ctx, rc, std::string("cannot write ") + path);
     if (rc) return set_error(ctx, rc, "dmap2pcl: map has no positive disparity");
     return MVSV_OK;
+    }());
 }
 
 // ---- rectification ------------------------------------------
@@ -652,6 +659,7 @@ int mvsv_resize(mvsv_ctx* ctx, const uint8_t* src, size_t ss, int sw, int sh, do
         ds < (size_t)dw)
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad resize arguments");
     DeviceGuard dev_guard(ctx->device);
+    return mark_last_use(ctx, [&]() -> int {
     const size_t in = (size_t)sw * sh, outb = (size_t)dw * dh;
     int rc;
     if ((rc = ensure(ctx, ctx->h_left, in, "resize staging")) ||
@@ -666,6 +674,7 @@ int mvsv_resize(mvsv_ctx* ctx, const uint8_t* src, size_t ss, int sw, int sh, do
                         "D2H image")))
         return rc;
     return check_hip(ctx, hipStreamSynchronize(s), "hipStreamSynchronize");
+    }());
 }
 
 // [Stereosystem::getRectifiedImagepair] src/Stereosystem.cpp:243-262
@@ -682,6 +691,7 @@ int mvsv_rectify_pair(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t*
     for (int i = 0; i < 4; i++)
         if (!maps[i]) return set_error(ctx, MVSV_E_INVALID_ARG, "null map");
     DeviceGuard dev_guard(ctx->device);
+    return mark_last_use(ctx, [&]() -> int {
     const size_t px = (size_t)W * H;
     int rc;
     if ((rc = ensure(ctx, ctx->h_left, 2 * px, "rectify staging")) ||
@@ -715,5 +725,6 @@ int mvsv_rectify_pair(mvsv_ctx* ctx, const uint8_t* L, size_t ls, const uint8_t*
                                                   ch, hipMemcpyDeviceToHost, s), "D2H image")))
             return rc;
     return check_hip(ctx, hipStreamSynchronize(s), "hipStreamSynchronize");
+    }());
 }
 

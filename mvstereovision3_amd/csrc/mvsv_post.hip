@@ -584,6 +584,16 @@ int resize_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_t sf
     int dw, dh;
     if (resize_size(sw, sh, fx, fy, &dw, &dh)) return set_error(ctx, MVSV_E_INVALID_ARG, "bad resize factors");
     if (ds < (size_t)dw) return set_error(ctx, MVSV_E_INVALID_ARG, "resize destination stride smaller than width");
+    if (dw == sw && dh == sh) {
+        // [OpenCV 3.4 resize] dsize == ssize: src.copyTo(dst), whatever fx, fy
+        for (int f = 0; f < n; f++) {
+            const int rc = check_hip(ctx, hipMemcpy2DAsync(dst + (size_t)f * dfs, ds, src + (size_t)f * sfs, ss, sw, sh,
+                                                           hipMemcpyDeviceToDevice, ctx->stream),
+                                     "resize copy");
+            if (rc) return rc;
+        }
+        return MVSV_OK;
+    }
     const double scale_x = 1.0 / fx, scale_y = 1.0 / fy;
     const double isx = std::nearbyint(scale_x), isy = std::nearbyint(scale_y);
     const bool area2 = std::fabs(scale_x - isx) < DBL_EPSILON && std::fabs(scale_y - isy) < DBL_EPSILON &&

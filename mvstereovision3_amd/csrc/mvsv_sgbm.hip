@@ -391,7 +391,8 @@ template <int NR, int STG, int PPC>
 __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4))) void sgbm_cost2_kernel(const uint64_t* __restrict__ pre,
                                                                    int W, int H, SgbmEff e, int TY,
                                                                    int16_t* __restrict__ C,
-                                                                   uint8_t* __restrict__ Rv)
+                                                                   uint8_t* __restrict__ Rv,
+                                                                   uint16_t* __restrict__ Mv)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int SH2 = NR / 2;
@@ -609,25 +610,57 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                     ov[i] = pin ? p2x2 : pk_add_u16(p2x2, csum[i]);
                     if (emit && i < nout) orow[i * PP] = ov[i];
                 }
-                // residual plane: the lanes of a column lane hold its pixel's
-                // D costs (PP <= 64 lanes, one aligned segment of the wave);
-                // the four columns' minima in two packed segment reductions
+                // residual plane + per-pixel minimum: the lanes of a column
+                // lane hold its pixel's D costs (PP <= 64 lanes, an aligned
+                // segment of the wave).  The four columns' minima: pairs
+                // (m0, m1) and (m2, m3) per lane, then one transposing step
+                // (even lanes keep reducing (m0, m1), odd lanes (m2, m3)) and
+                // five parity-preserving butterfly steps on a single dword.
                 if (Rv && emit) {
-                    const uint32_t m01 = seg_min_u16x2(
-                        pk_min_u16(__builtin_amdgcn_perm(ov[1], ov[0], 0x05040100u),
-                                   __builtin_amdgcn_perm(ov[1], ov[0], 0x07060302u)), PP);
-                    const uint32_t m23 = seg_min_u16x2(
-                        pk_min_u16(__builtin_amdgcn_perm(ov[3], ov[2], 0x05040100u),
-                                   __builtin_amdgcn_perm(ov[3], ov[2], 0x07060302u)), PP);
+                    uint32_t A = pk_min_u16(__builtin_amdgcn_perm(ov[1], ov[0], 0x05040100u),
+                                            __builtin_amdgcn_perm(ov[1], ov[0], 0x07060302u));
+                    uint32_t B = pk_min_u16(__builtin_amdgcn_perm(ov[3], ov[2], 0x05040100u),
+                                            __builtin_amdgcn_perm(ov[3], ov[2], 0x07060302u));
+                    const bool odd = (p & 1) != 0;
+                    uint32_t X = pk_min_u16(odd ? B : A,
+                                            (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? A : B), 0xB1, 0xf, 0xf, false));
+                    X = pk_min_u16(X, (uint32_t)__builtin_amdgcn_mov_dpp((int)X, 0x4E, 0xf, 0xf, false));   // lane ^ 2
+                    X = pk_min_u16(X, (uint32_t)__builtin_amdgcn_mov_dpp((int)X, 0x124, 0xf, 0xf, false));  // row_ror:4
+                    X = pk_min_u16(X, (uint32_t)__builtin_amdgcn_mov_dpp((int)X, 0x128, 0xf, 0xf, false));  // row_ror:8
+                    if (PP >= 32) {
+                        const auto sw = __builtin_amdgcn_permlane16_swap(X, X, false, false);
+                        X = pk_min_u16(sw[0], sw[1]);
+                    }
+                    if (PP >= 64) {
+                        const auto sw = __builtin_amdgcn_permlane32_swap(X, X, false, false);
+                        X = pk_min_u16(sw[0], sw[1]);
+                    }
+                    const uint32_t Y = (uint32_t)__builtin_amdgcn_mov_dpp((int)X, 0xB1, 0xf, 0xf, false);
+                    A = odd ? Y : X;  // (m0, m1) in every lane
+                    B = odd ? X : Y;  // (m2, m3)
+                    // per-pixel minimum (the final kernel's absolute cost base)
+                    if (p == 0) {
+                        uint16_t* mrow = Mv + (size_t)(orow - (uint32_t*)C) / PP;
+                        const uint32_t mv[kCost2Run] = {A, A >> 16, B, B >> 16};
+#pragma unroll
+                        for (int i = 0; i < kCost2Run; i++)
+                            if (i < nout) mrow[i] = (uint16_t)mv[i];
+                    }
+                    // R = min(C - m, 2 P2) + P2 = min(C - (m - P2), 3 P2), byte
+                    // = R(2p) + 16 R(2p + 1) (one v_dot2_u32_u16)
+                    const uint32_t Am = pk_sub_u16(A, p2x2), Bm = pk_sub_u16(B, p2x2);
                     const uint32_t mm[kCost2Run] = {
-                        __builtin_amdgcn_perm(m01, m01, 0x01000100u), __builtin_amdgcn_perm(m01, m01, 0x03020302u),
-                        __builtin_amdgcn_perm(m23, m23, 0x01000100u), __builtin_amdgcn_perm(m23, m23, 0x03020302u)};
+                        __builtin_amdgcn_perm(Am, Am, 0x01000100u), __builtin_amdgcn_perm(Am, Am, 0x03020302u),
+                        __builtin_amdgcn_perm(Bm, Bm, 0x01000100u), __builtin_amdgcn_perm(Bm, Bm, 0x03020302u)};
                     uint8_t* rrow = Rv + (orow - (uint32_t*)C);  // byte (pixel, pair) = dword (pixel, pair) of C
-                    const uint32_t p2x4 = pk_add_u16(p2x2, p2x2);
+                    const uint32_t p2x3 = pk_add_u16(pk_add_u16(p2x2, p2x2), p2x2);
+                    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+                    const u16x2 nib = {1, 16};
 #pragma unroll
                     for (int i = 0; i < kCost2Run; i++) {
-                        const uint32_t r = pk_add_u16(pk_min_u16(pk_sub_u16(ov[i], mm[i]), p2x4), p2x2);
-                        if (i < nout) rrow[i * PP] = (uint8_t)(r | (r >> 12));
+                        const uint32_t r = pk_min_u16(pk_sub_u16(ov[i], mm[i]), p2x3);
+                        if (i < nout)
+                            rrow[i * PP] = (uint8_t)__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, r), nib, 0u, false);
                     }
                 }
             }
@@ -643,7 +676,8 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
 // A pixel's residual (when Rv != nullptr) depends only on its own D costs, so
 // a copied cost vector carries its residual bytes along (P2 everywhere: P2).
 __global__ __launch_bounds__(256) void sgbm_cost_fixup_col0_kernel(int16_t* __restrict__ C, int H,
-                                                                   SgbmEff e, uint8_t* __restrict__ Rv)
+                                                                   SgbmEff e, uint8_t* __restrict__ Rv,
+                                                                   uint16_t* __restrict__ Mv)
 {
     const int y = 1 + blockIdx.x;
     const int f = blockIdx.y;
@@ -656,6 +690,8 @@ __global__ __launch_bounds__(256) void sgbm_cost_fixup_col0_kernel(int16_t* __re
         uint8_t* rrow = Rf + (size_t)y * W1 * (D / 2);
         for (int k = threadIdx.x; k < D / 2; k += blockDim.x)
             rrow[k] = e.fullDP ? (uint8_t)(e.P2 * 0x11) : Rf[k];
+        uint16_t* Mf = Mv + (size_t)f * H * W1;
+        if (threadIdx.x == 0) Mf[(size_t)y * W1] = e.fullDP ? (uint16_t)e.P2 : Mf[0];
     }
 }
 
@@ -664,7 +700,8 @@ __global__ __launch_bounds__(256) void sgbm_cost_fixup_col0_kernel(int16_t* __re
 // multiple of 16, so a 16-byte chunk never straddles two columns.
 __global__ __launch_bounds__(256) void sgbm_cost_fixup_bottom_kernel(int16_t* __restrict__ C, int H,
                                                                      SgbmEff e, int ylast, int ybot,
-                                                                     uint8_t* __restrict__ Rv)
+                                                                     uint8_t* __restrict__ Rv,
+                                                                     uint16_t* __restrict__ Mv)
 {
     const int D = e.D, W1 = e.W1;
     const size_t chunk = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // 8 elements each
@@ -688,6 +725,11 @@ __global__ __launch_bounds__(256) void sgbm_cost_fixup_bottom_kernel(int16_t* __
         uint32_t* Rf = (uint32_t*)(Rv + (size_t)f * H * (rowlen / 2));
         Rf[(size_t)y * (rowlen / 8) + chunk] =
             e.fullDP ? (uint32_t)e.P2 * 0x11111111u : Rf[(col0 ? 0 : (size_t)ylast * (rowlen / 8)) + chunk];
+        if (chunk * 8 % D == 0) {  // the first chunk of a pixel carries its minimum
+            uint16_t* Mf = Mv + (size_t)f * H * W1;
+            const size_t x = chunk * 8 / D;
+            Mf[(size_t)y * W1 + x] = e.fullDP ? (uint16_t)e.P2 : Mf[col0 ? 0 : (size_t)ylast * W1 + x];
+        }
     }
 }
 
@@ -2092,14 +2134,28 @@ __device__ __forceinline__ uint32_t pk_mad_u16_clamp(uint32_t a, uint32_t b, uin
 // NACC accumulator planes (A + i * plane) hold the summed deltas of disjoint
 // direction groups written by concurrent passes; their sum is the S input.
 // UQ: uniquenessRatio > 0.
-template <int NP, int NACC, typename AccT, bool UQ, int LPR, bool NOWRAP = false>
+// RESF (round 4; uniquenessRatio == 0 only, no-wrap regime): the recurrence
+// and the WTA run on the residual plane R instead of C.  With C' = C - m
+// (m = the pixel's minimum cost, Mv) and C'' = min(C', 2 P2) = R - P2, the
+// step computes S'' = n C'' + sum of deltas (n = 8 or 5 directions);
+// S = min(n (m - P2) + S', MAX_COST) has the same argmin and ties as S'' (the
+// minimum of S' is <= n P2 < 2 n P2 <= S'' of any clamped d), and with
+// uniquenessRatio 0 no d is ever rejected.  Only the sub-pixel fit needs
+// exact S(best -+ 1): where S'' >= 2 n P2 the residual
+// may be clamped and the flush loads C(best -+ 1) from the cost volume (one
+// 2-byte gather per pixel, issued one flush ahead of its use so the prefetch
+// loads are never waited for).
+template <int NP, int NACC, typename AccT, bool UQ, int LPR, bool NOWRAP = false, bool RESF = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 : 2))) void sgbm_final16_kernel(const int16_t* __restrict__ C,
                                                          const AccT* __restrict__ A, size_t plane,
                                                          int H, int W, SgbmEff e,
                                                          int16_t* __restrict__ raw,
                                                          uint32_t* __restrict__ keys,
-                                                         int16_t* __restrict__ dummy)
+                                                         int16_t* __restrict__ dummy,
+                                                         const uint8_t* __restrict__ Rv,
+                                                         const uint16_t* __restrict__ Mv)
 {
+    static_assert(!(RESF && UQ), "the residual final kernel needs uniquenessRatio 0");
     using AR = AccRaw<NP, AccT>;
     constexpr int NW = AR::NW;
     // 32 lanes per row: twice the waves, so a shallower prefetch keeps the
@@ -2154,7 +2210,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     for (int p = 0; p < NP; p++) dpair[p] = (uint32_t)(d0 + 2 * p) | ((uint32_t)(d0 + 2 * p + 1) << 16);
     int minp = 0;
 
-    Vec<NP> cb[PF];
+    // cost words per prefetch slot: NP packed pairs of C, or the lane's 2 NP
+    // residual nibbles (NP bytes, one word)
+    constexpr int NCW = RESF ? 1 : NP;
+    uint32_t cw[PF][NCW];
     uint32_t ab[PF][NACC][NW];
     // Buffer loads: one descriptor per volume over the wave's RPW rows, the
     // lane's row/disparity offset in a VGPR and the column (x = W1 - 1 - t)
@@ -2163,19 +2222,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     const size_t rbase = f * frame + (size_t)ybase * W1 * D;
     const uint32_t loff = (uint32_t)((y - ybase) * W1 * D + d0);  // elements, even
     constexpr uint32_t kAccNum = (uint32_t)sizeof(AccT), kAccDen = AccEpu<AccT>::v;  // bytes per element
-    const int nrec_c = RPW * W1 * D * 2;
+    constexpr uint32_t kCNum = RESF ? 1u : 4u, kCDen = 2u;  // cost input bytes per element: 1/2 or 2
+    const int nrec_c = (int)((uint32_t)(RPW * W1 * D) * kCNum / kCDen);
     const int nrec_a = (int)((uint32_t)(RPW * W1 * D) * kAccNum / kAccDen);
+    const void* cbase = RESF ? (const void*)(Rv + rbase / 2) : (const void*)(C + rbase);
     const __amdgpu_buffer_rsrc_t rc_c =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(C + rbase), (short)0, nrec_c, kBufWord3);
+        __builtin_amdgcn_make_buffer_rsrc((void*)cbase, (short)0, nrec_c, kBufWord3);
     __amdgpu_buffer_rsrc_t rc_a[NACC];
 #pragma unroll
     for (int i = 0; i < NACC; i++)
         rc_a[i] = __builtin_amdgcn_make_buffer_rsrc(
             (void*)acc_add(A, (ptrdiff_t)(rbase + (size_t)i * plane)), (short)0, nrec_a, kBufWord3);
-    const uint32_t vo_c = 2u * loff, vo_a = loff * kAccNum / kAccDen;
+    const uint32_t vo_c = loff * kCNum / kCDen, vo_a = loff * kAccNum / kAccDen;
     auto prefetch = [&](int j, ptrdiff_t t) {
         const uint32_t xd = (uint32_t)((W1 - 1 - (int)t) * D);
-        buf_words<4 * NP>(rc_c, vo_c, 2u * xd, cb[j].v);
+        buf_words<(int)(2 * NP * kCNum / kCDen)>(rc_c, vo_c, xd * kCNum / kCDen, cw[j]);
 #pragma unroll
         for (int i = 0; i < NACC; i++)
             buf_words<2 * NP * kAccNum / kAccDen>(rc_a[i], vo_a, xd * kAccNum / kAccDen, ab[j][i]);
@@ -2193,8 +2254,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     auto body = [&](int s, int j) {
         const uint32_t delta2 = sgm_delta2<NOWRAP>(minp, e.P2);
         uint32_t c[NP], ln[NP], st[NP], acc[NP], tt[NP];
+        if constexpr (RESF) {
+            CostIn<NP, true> ci;
+            ci.w[0] = cw[j][0];
+            ci.get(c);
+        } else {
 #pragma unroll
-        for (int p = 0; p < NP; p++) c[p] = cb[j].v[p];
+            for (int p = 0; p < NP; p++) c[p] = cw[j][p];
+        }
         sgm_step_seg_t<NP, LPR, NOWRAP>(lp, delta2, p1x2, c, ln, tt, seg_first, seg_last);
         minp = seg_min_i32<LPR>(lane_min_row<NP>(ln));
         AR::template combine<NACC>(ab[j], acc);
@@ -2250,18 +2317,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     // its dummy slot, a rejected column rewrites INVALID, and an atomicMin
     // that must not count carries the all-ones key (a no-op).
     int16_t* dslot = dummy + (blockIdx.x & 63) * 64 + lane;
-    auto flush = [&](int s0, int cnt) {
-        const int s = s0 + rl;
-        const bool own = exists && rl < cnt;
-        const uint2 rec = recs[rl];
-        const uint32_t kK = rec.x & 0x7fffffffu, kS = rec.y;
-        const int kRej = (int)(rec.x >> 31);
-        const int minS = (int)(kK >> 16);
-        const int sub = (int)(kK & 0xffffu);
-        int best = lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
+    // store + right-view key of one finished column (x, exact minS, Sm, Sp)
+    auto finish = [&](bool own, int x, int best, int minS, int Sm, int Sp, int kRej) {
         if (minS >= kMaxCost) best = -1;  // no strict minimum below MAX_COST
-        const int Sm = (int)(int16_t)(kS & 0xffffu), Sp = (int)(int16_t)(kS >> 16);
-        const int x = W1 - 1 - s;
         const int den = max(Sm + Sp - 2 * minS, 1);
         const int frac = ((Sm - Sp) * kDispScale + den) / (den * 2);
         // arithmetic mask, not a select: the division stays unconditional (no
@@ -2274,6 +2332,66 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
         atomicMin(krow + clampi(x2, 0, W - 1),
                   hit ? (((uint32_t)minS << 16) | (uint32_t)(0xffff - x)) : 0xffffffffu);
     };
+    auto flush = [&](int s0, int cnt) {
+        const int s = s0 + rl;
+        const bool own = exists && rl < cnt;
+        const uint2 rec = recs[rl];
+        const uint32_t kK = rec.x & 0x7fffffffu, kS = rec.y;
+        const int kRej = (int)(rec.x >> 31);
+        const int minS = (int)(kK >> 16);
+        const int sub = (int)(kK & 0xffffu);
+        const int best = lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
+        const int Sm = (int)(int16_t)(kS & 0xffffu), Sp = (int)(int16_t)(kS >> 16);
+        finish(own, W1 - 1 - s, best, minS, Sm, Sp, kRej);
+    };
+    // RESF: a flush reads its columns' records and issues their loads (the
+    // pixel minimum, C(best -+ 1) where the residual may be clamped); the next
+    // flush (or the row end) finishes them.  Pending state per lane: the
+    // record and three loaded values (the column and ownership follow from
+    // the pending flush's first step and count, wave-uniform).
+    struct Pend {
+        uint2 rec;
+        int mC, cm, cp;
+    } pend{};
+    int pend_s0 = 0, pend_cnt = 0;
+    const int16_t* crow = C + f * frame + (size_t)y * W1 * D;
+    const uint16_t* mrowp = RESF ? Mv + ((size_t)f * H + y) * W1 : nullptr;
+    const int ndir = e.fullDP ? 8 : 5;
+    const int clampS = ndir * 2 * e.P2;  // S'' >= this: C'' may be the clamp value
+    auto rec_best = [&](uint32_t kK) {
+        const int sub = (int)(kK & 0xffffu);
+        return lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
+    };
+    auto finish_res = [&](const Pend& q, int s0, int cnt) {
+        const uint32_t kK = q.rec.x & 0x7fffffffu;
+        const int base = ndir * (q.mC - e.P2);  // S = min(base + S', MAX_COST)
+        auto exact = [&](int Spp, int cv) -> int {
+            // S'' = ndir C'' + deltas; where the flush loaded C(d) (S'' >=
+            // clampS: cv is exact, else a placeholder) replace C'' = min(C', 2 P2)
+            // by C'
+            const int c1 = Spp >= clampS ? cv - q.mC : 0;
+            return min(base + Spp + ndir * (c1 - min(c1, 2 * e.P2)), kMaxCost);
+        };
+        const int Sm = exact((int)(q.rec.y & 0xffffu), q.cm), Sp = exact((int)(q.rec.y >> 16), q.cp);
+        finish(exists && rl < cnt, W1 - 1 - (s0 + rl), rec_best(kK), min(base + (int)(kK >> 16), kMaxCost),
+               Sm, Sp, 0);
+    };
+    auto flush_res = [&](int s0, int cnt) {
+        Pend q;
+        const bool own = exists && rl < cnt;
+        q.rec = recs[rl];
+        const int best = rec_best(q.rec.x & 0x7fffffffu);
+        const int xc = own ? W1 - 1 - (s0 + rl) : 0;
+        q.mC = mrowp[xc];
+        const int bm = max(best - 1, 0), bp = min(best + 1, D - 1);
+        // one shared address for the lanes that need no exact cost
+        q.cm = crow[(own && (int)(q.rec.y & 0xffffu) >= clampS) ? (size_t)xc * D + bm : 0];
+        q.cp = crow[(own && (int)(q.rec.y >> 16) >= clampS) ? (size_t)xc * D + bp : 0];
+        finish_res(pend, pend_s0, pend_cnt);  // the previous flush's columns (none the first time)
+        pend = q;
+        pend_s0 = s0;
+        pend_cnt = cnt;
+    };
     int s = 0;
     for (; s + LPR <= W1; s += LPR) {
 #pragma unroll
@@ -2281,7 +2399,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
             body(s + j, j % PF);
             prefetch(j % PF, min(s + j + PF, W1 - 1));
         }
-        flush(s, LPR);
+        if constexpr (RESF)
+            flush_res(s, LPR);
+        else
+            flush(s, LPR);
     }
     const int rem = W1 - s;
 #pragma unroll
@@ -2291,7 +2412,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
             prefetch(j % PF, min(s + j + PF, W1 - 1));
         }
     }
-    if (rem > 0) flush(s, rem);
+    if constexpr (RESF) {
+        if (rem > 0) flush_res(s, rem);
+        finish_res(pend, pend_s0, pend_cnt);
+    } else {
+        if (rem > 0) flush(s, rem);
+    }
     __threadfence_block();
     __syncthreads();
     if (!exists) return;
@@ -2502,9 +2628,10 @@ __global__ void fill_s16_kernel(int16_t* __restrict__ out, size_t os, size_t ofs
 }
 
 // sheared-strip schedule: enabled, and int32 element offsets cover a frame
-template <int NP, int NACC, typename AccT, bool NW = false>
+template <int NP, int NACC, typename AccT, bool NW = false, bool RES = false>
 void launch_final16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv,
-                    const AccT* Av, size_t plane, int16_t* raw)
+                    const AccT* Av, size_t plane, int16_t* raw, const void* Rv = nullptr,
+                    const uint16_t* Mv = nullptr)
 {
     // NP: disparity pairs per lane at 16 lanes per row.  D >= 128: 32 lanes per
     // row (half the pairs per lane, twice the rows in flight per SIMD); a lane
@@ -2513,14 +2640,23 @@ void launch_final16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const 
     constexpr int NPL = NP * 16 / LPR;
     constexpr int RPW = 64 / LPR;
     const dim3 grid((H + RPW - 1) / RPW, n);
+    uint32_t* keys = (uint32_t*)ctx->keys.ptr;
+    int16_t* dummy = (int16_t*)ctx->dummy.ptr;
+    if constexpr (RES) {
+        // residual plane: WTA on R, exact costs gathered for the sub-pixel fit
+        // (uniquenessRatio 0 only: a ratio test needs every exact cost)
+        if (e.uniq == 0) {
+            hipLaunchKernelGGL((sgbm_final16_kernel<NPL, NACC, AccT, false, LPR, NW, true>), grid, dim3(64), 0,
+                               ctx->stream, Cv, Av, plane, H, W, e, raw, keys, dummy, (const uint8_t*)Rv, Mv);
+            return;
+        }
+    }
     if (e.uniq > 0)
         hipLaunchKernelGGL((sgbm_final16_kernel<NPL, NACC, AccT, true, LPR, NW>), grid, dim3(64), 0,
-                           ctx->stream, Cv, Av, plane, H, W, e, raw, (uint32_t*)ctx->keys.ptr,
-                           (int16_t*)ctx->dummy.ptr);
+                           ctx->stream, Cv, Av, plane, H, W, e, raw, keys, dummy, nullptr, nullptr);
     else
         hipLaunchKernelGGL((sgbm_final16_kernel<NPL, NACC, AccT, false, LPR, NW>), grid, dim3(64), 0,
-                           ctx->stream, Cv, Av, plane, H, W, e, raw, (uint32_t*)ctx->keys.ptr,
-                           (int16_t*)ctx->dummy.ptr);
+                           ctx->stream, Cv, Av, plane, H, W, e, raw, keys, dummy, nullptr, nullptr);
 }
 
 // Every cost C = P2 + (box sum of blockSize^2 BT costs, each <= 2*ftzero + 63),
@@ -2710,7 +2846,7 @@ int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const void* Cv, Ac
 // final kernel the cost volume Cv.
 template <int NP, typename AccT, bool NW, bool RES = false>
 int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, const void* Cin,
-                     AccT* Av, size_t plane, int16_t* raw)
+                     AccT* Av, size_t plane, int16_t* raw, const uint16_t* Mv = nullptr)
 {
     hipStream_t s = ctx->stream;
     int rc;
@@ -2761,9 +2897,9 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
     }
     StageTimer tm(ctx, kStageFinal);
     if (npass == 2)
-        launch_final16<NP, 3, AccT, NW>(ctx, n, H, W, e, Cv, Av, plane, raw);
+        launch_final16<NP, 3, AccT, NW, RES>(ctx, n, H, W, e, Cv, Av, plane, raw, Cin, Mv);
     else
-        launch_final16<NP, 2, AccT, NW>(ctx, n, H, W, e, Cv, Av, plane, raw);
+        launch_final16<NP, 2, AccT, NW, RES>(ctx, n, H, W, e, Cv, Av, plane, raw, Cin, Mv);
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels (sheared strips)");
 }
 
@@ -2840,7 +2976,7 @@ int launch_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* 
 
 template <int NP, typename AccT, bool NW, bool RES = false>
 int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, const void* Cin,
-                      AccT* Av, int16_t* raw)
+                      AccT* Av, int16_t* raw, const uint16_t* Mv = nullptr)
 {
     static const int dirs_sgbm[4][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}};
     static const int dirs_hh[7][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}, {1, -1}, {0, -1}, {-1, -1}};
@@ -2861,9 +2997,9 @@ int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int1
     }
     StageTimer tm(ctx, kStageFinal);
     if (ndir == 7)
-        launch_final16<NP, 7, AccT, NW>(ctx, n, H, W, e, Cv, Av, plane, raw);
+        launch_final16<NP, 7, AccT, NW, RES>(ctx, n, H, W, e, Cv, Av, plane, raw, Cin, Mv);
     else
-        launch_final16<NP, 4, AccT, NW>(ctx, n, H, W, e, Cv, Av, plane, raw);
+        launch_final16<NP, 4, AccT, NW, RES>(ctx, n, H, W, e, Cv, Av, plane, raw, Cin, Mv);
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels (directions side by side)");
 }
 
@@ -2871,7 +3007,7 @@ int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int1
 // set in the no-wrap regime with 3 * P2 <= 15, use_residual)
 template <int NP>
 int launch_paths16_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv,
-                       const uint8_t* Rv, void* Av, int16_t* raw)
+                       const uint8_t* Rv, const uint16_t* Mv, void* Av, int16_t* raw)
 {
     if (path_schedule(ctx, e, H, n) == 2) {
         int rc;
@@ -2882,7 +3018,7 @@ int launch_paths16_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int
         if (e.P2 <= 15) {
             if (sgbm_no_wrap(e)) {
                 if constexpr (NP <= 4)
-                    if (Rv) return launch_paths_dirs<NP, nib2_t, true, true>(ctx, n, H, W, e, Cv, Rv, (nib2_t*)Av, raw);
+                    if (Rv) return launch_paths_dirs<NP, nib2_t, true, true>(ctx, n, H, W, e, Cv, Rv, (nib2_t*)Av, raw, Mv);
                 return launch_paths_dirs<NP, nib2_t, true>(ctx, n, H, W, e, Cv, Cv, (nib2_t*)Av, raw);
             }
             return launch_paths_dirs<NP, nib2_t, false>(ctx, n, H, W, e, Cv, Cv, (nib2_t*)Av, raw);
@@ -2898,7 +3034,7 @@ int launch_paths16_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int
         const size_t plane = (size_t)n * H * e.W1 * e.D;
         if (sgbm_no_wrap(e)) {
             if constexpr (NP <= 4)
-                if (Rv) return launch_paths_tri<NP, nib2_t, true, true>(ctx, n, H, W, e, Cv, Rv, (nib2_t*)Av, plane, raw);
+                if (Rv) return launch_paths_tri<NP, nib2_t, true, true>(ctx, n, H, W, e, Cv, Rv, (nib2_t*)Av, plane, raw, Mv);
             return launch_paths_tri<NP, nib2_t, true>(ctx, n, H, W, e, Cv, Cv, (nib2_t*)Av, plane, raw);
         }
         return launch_paths_tri<NP, nib2_t, false>(ctx, n, H, W, e, Cv, Cv, (nib2_t*)Av, plane, raw);
@@ -2917,7 +3053,7 @@ int launch_paths_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
 
 }  // namespace
 
-using Cost2Kern = void (*)(const uint64_t*, int, int, SgbmEff, int, int16_t*, uint8_t*);
+using Cost2Kern = void (*)(const uint64_t*, int, int, SgbmEff, int, int16_t*, uint8_t*, uint16_t*);
 template <int STG, int PPC>
 static Cost2Kern cost2_pick_nr(int nr)
 {
@@ -2946,7 +3082,7 @@ static Cost2Kern cost2_pick(int nr, int stg, int ppc)
 // is written by the register-ring kernel only: the LDS-ring fallback sets it
 // to nullptr, and the direction passes then read C.
 static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int TY,
-                       const uint64_t* pre, int16_t* Cv, uint8_t** Rv, bool* pinned_hh)
+                       const uint64_t* pre, int16_t* Cv, uint8_t** Rv, uint16_t* Mv, bool* pinned_hh)
 {
     *pinned_hh = false;
     hipStream_t s = ctx->stream;
@@ -2972,7 +3108,7 @@ static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int
             {
                 StageTimer tm(ctx, kStageCost);
                 hipLaunchKernelGGL(kern, grid2, dim3(kCost2Threads), l2.bytes, s, pre, W, H, e, TY,
-                                   Cv, *Rv);
+                                   Cv, *Rv, Mv);
             }
             *pinned_hh = e.fullDP != 0;  // MODE_HH fix-up rows/column written by the kernel
             return check_hip(ctx, hipGetLastError(), "sgbm cost kernel");
@@ -3027,10 +3163,14 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
         return rc;
     if ((rc = ensure(ctx, ctx->raw, (size_t)n * plane * 2, "sgbm raw disparity"))) return rc;
     // residual plane for the direction passes (0.5 byte per cost instead of 2)
+    // + the per-pixel cost minimum (u16 per cost column) behind it
     uint8_t* Rv = nullptr;
+    uint16_t* Mv = nullptr;
     if (use_residual(ctx, e, sched)) {
-        if ((rc = ensure(ctx, ctx->cres, (size_t)n * vol / 2, "sgbm cost residual plane"))) return rc;
+        const size_t rbytes = (n * vol / 2 + 255) & ~(size_t)255;
+        if ((rc = ensure(ctx, ctx->cres, rbytes + (size_t)n * e.W1 * H * 2, "sgbm cost residual plane"))) return rc;
         Rv = (uint8_t*)ctx->cres.ptr;
+        Mv = (uint16_t*)(Rv + rbytes);
     }
     uint64_t* pre = (uint64_t*)ctx->pre.ptr;
     int16_t* Cv = (int16_t*)ctx->cost.ptr;
@@ -3073,7 +3213,7 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
         }
     }
     bool pinned_hh = false;
-    if ((rc = launch_cost(ctx, n, W, H, e, TY, pre, Cv, &Rv, &pinned_hh))) return rc;
+    if ((rc = launch_cost(ctx, n, W, H, e, TY, pre, Cv, &Rv, Mv, &pinned_hh))) return rc;
 
     const int ybot = std::max(H - e.SH2, 1);     // first row that is never recomputed
     const int ylast = std::max(H - e.SH2 - 1, 0);  // last recomputed row
@@ -3085,11 +3225,11 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
         // bottom kernel (the rows are disjoint).
         const bool fix = (e.variant & MVSV_VARIANT_FIRSTCOL_FIX) != 0;
         if (ybot > 1 && !fix)
-            hipLaunchKernelGGL(sgbm_cost_fixup_col0_kernel, dim3(ybot - 1, n), dim3(256), 0, s, Cv, H, e, Rv);
+            hipLaunchKernelGGL(sgbm_cost_fixup_col0_kernel, dim3(ybot - 1, n), dim3(256), 0, s, Cv, H, e, Rv, Mv);
         if (ybot < H) {
             const size_t chunks = ((size_t)e.W1 * e.D + 7) / 8;
             hipLaunchKernelGGL(sgbm_cost_fixup_bottom_kernel, dim3((unsigned)((chunks + 255) / 256), H - ybot, n),
-                               dim3(256), 0, s, Cv, H, e, ylast, ybot, Rv);
+                               dim3(256), 0, s, Cv, H, e, ylast, ybot, Rv, Mv);
         }
         if ((rc = check_hip(ctx, hipGetLastError(), "sgbm cost fixup"))) return rc;
     }
@@ -3098,10 +3238,10 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     const bool wide = ctx->path16 && (e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256);
     if (wide) {
         switch (e.D) {
-        case 32: rc = launch_paths16_acc<1>(ctx, n, H, W, e, Cv, Rv, Sv, raw); break;
-        case 64: rc = launch_paths16_acc<2>(ctx, n, H, W, e, Cv, Rv, Sv, raw); break;
-        case 128: rc = launch_paths16_acc<4>(ctx, n, H, W, e, Cv, Rv, Sv, raw); break;
-        default: rc = launch_paths16_acc<8>(ctx, n, H, W, e, Cv, nullptr, Sv, raw); break;
+        case 32: rc = launch_paths16_acc<1>(ctx, n, H, W, e, Cv, Rv, Mv, Sv, raw); break;
+        case 64: rc = launch_paths16_acc<2>(ctx, n, H, W, e, Cv, Rv, Mv, Sv, raw); break;
+        case 128: rc = launch_paths16_acc<4>(ctx, n, H, W, e, Cv, Rv, Mv, Sv, raw); break;
+        default: rc = launch_paths16_acc<8>(ctx, n, H, W, e, Cv, nullptr, nullptr, Sv, raw); break;
         }
     } else if (np == 1) rc = launch_paths_acc<1>(ctx, n, H, W, e, Cv, Sv, raw);
     else if (np == 2) rc = launch_paths_acc<2>(ctx, n, H, W, e, Cv, Sv, raw);

@@ -350,6 +350,7 @@ int mvsv_mean_disparity_grid(mvsv_ctx* ctx, const int16_t* dmap, size_t st, int 
     if (!dmap || !means || W <= 0 || H <= 0 || st < (size_t)W)
         return set_error(ctx, MVSV_E_INVALID_ARG, "bad mean-grid arguments");
     DeviceGuard dev_guard(ctx->device);
+    return mark_last_use(ctx, [&]() -> int {  // every exit after an enqueue
     const size_t px = (size_t)W * H;
     int rc;
     if ((rc = ensure(ctx, ctx->h_out, px * 2 + 4 + 81 * sizeof(float), "grid staging"))) return rc;
@@ -363,4 +364,5 @@ int mvsv_mean_disparity_grid(mvsv_ctx* ctx, const int16_t* dmap, size_t st, int 
                         "D2H means")))
         return rc;
     return check_hip(ctx, hipStreamSynchronize(s), "hipStreamSynchronize");
+    }());
 }

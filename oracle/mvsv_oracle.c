@@ -928,6 +928,10 @@ void orc_resize_linear(const uint8_t* src, ptrdiff_t ss, int sw, int sh, double 
     *out_w = dw;
     *out_h = dh;
     if (!dst) return;
+    if (dw == sw && dh == sh) { /* dsize == ssize: src.copyTo(dst) */
+        for (int y = 0; y < sh; y++) memcpy(dst + (ptrdiff_t)y * ds, src + (ptrdiff_t)y * ss, (size_t)sw);
+        return;
+    }
     const double scale_x = 1.0 / fx, scale_y = 1.0 / fy;
     const int isx = orc_round_d(scale_x), isy = orc_round_d(scale_y);
     const int area_fast = fabs(scale_x - isx) < DBL_EPSILON && fabs(scale_y - isy) < DBL_EPSILON;

@@ -9,7 +9,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 CASES = [((240, 376), 0.5), ((241, 377), 0.5), ((240, 376), 0.75), ((37, 53), 1.5), ((480, 640), 0.3),
-         ((5, 7), 0.5), ((96, 200), 2.0), ((33, 40), 0.6), ((64, 64), 1.0), ((17, 300), 0.25)]
+         ((5, 7), 0.5), ((96, 200), 2.0), ((33, 40), 0.6), ((64, 64), 1.0), ((17, 300), 0.25),
+         ((600, 600), 1.0005)]  # not 1, but rounds back to the same size: OpenCV copies
 
 
 @pytest.mark.parametrize("shape,f", CASES)

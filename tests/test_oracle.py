@@ -182,6 +182,10 @@ def test_oracle_resize_linear_properties(oracle):
     rs = np.random.RandomState(3)
     a = rs.randint(0, 256, (37, 53)).astype(np.uint8)
     assert np.array_equal(oracle.resize_linear(a, 1.0, 1.0), a)
+    # a factor that rounds back to the input size is a plain copy in OpenCV 3.4
+    # (resize: dsize == ssize -> src.copyTo(dst)), not a resampling
+    b = rs.randint(0, 256, (600, 600)).astype(np.uint8)
+    assert np.array_equal(oracle.resize_linear(b, 1.0005, 0.9995), b)
     h = oracle.resize_linear(a, 0.5, 0.5)
     assert h.shape == (18, 26)  # cvRound(18.5) = 18, cvRound(26.5) = 26 (half to even)
     q = a[:36, :52].astype(int)
