@@ -301,7 +301,7 @@ int mvsv_trim(mvsv_ctx* ctx)
     if (!ctx) return MVSV_E_INVALID_ARG;
     DeviceGuard dev_guard(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    DevBuf* all[] = {&ctx->pre, &ctx->cost, &ctx->cres, &ctx->agg, &ctx->raw, &ctx->uf_parent, &ctx->uf_size,
+    DevBuf* all[] = {&ctx->pre, &ctx->cost, &ctx->cres, &ctx->agg, &ctx->raw, &ctx->uf_parent, &ctx->uf_size, &ctx->uf_lroot, &ctx->uf_list,
                      &ctx->uf_tile, &ctx->tri_bnd, &ctx->status,
                      &ctx->dummy, &ctx->keys,
                      &ctx->bm_lf, &ctx->bm_rf, &ctx->bm_cost, &ctx->bm_sad, &ctx->h_left, &ctx->h_right,

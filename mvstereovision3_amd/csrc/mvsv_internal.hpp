@@ -89,7 +89,8 @@ struct mvsv_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // SGBM
-    mvsv::DevBuf pre, cost, cres, agg, raw, uf_parent, uf_size, uf_tile, dummy, keys, tri_bnd, status;
+    mvsv::DevBuf pre, cost, cres, agg, raw, uf_parent, uf_size, uf_tile, uf_lroot, uf_list, dummy, keys, tri_bnd, status;
+    bool uf_list_dirty = false;  // a speckle run launched its first stage but not its last
     // launch number of the last sheared-strip launch: its low 16 bits tag the
     // boundary granules (tri_bnd is re-zeroed whenever they wrap), all 32 bits
     // go into status[0] when that launch gives up a wait (no per-call reset)
@@ -194,6 +195,7 @@ int median3x3_device(mvsv_ctx* ctx, int n, const int16_t* src, size_t ss, size_t
                      const int* poison = nullptr, unsigned epoch = 0, int invalid = 0);
 int speckle_device(mvsv_ctx* ctx, int n, int16_t* img, size_t st, size_t fs, int W, int H,
                    int new_val, int max_size, int max_diff);
+
 int remap_device(mvsv_ctx* ctx, int n, const uint8_t* src, size_t ss, size_t sfs, int sw, int sh,
                  const float* mx, const float* my, size_t ms, uint8_t* dst, size_t ds, size_t dfs,
                  int dw, int dh);

@@ -8,6 +8,7 @@
 //     yields exactly the same components as OpenCV's raster-order flood fill.
 //   * MeanDisparityDetection grid   (src/MeanDisparityDetection.cpp:159-206,
 //     Utility::calcMeanDisparity src/utility.cpp:265-285)
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 
@@ -63,12 +64,64 @@ __global__ __launch_bounds__(256) void median3x3_kernel(const int16_t* __restric
     dst[f * dfs + (size_t)y * ds + x] = (int16_t)m;
 }
 
+// Two horizontally adjacent pixels per thread on packed int16 pairs
+// (v_pk_min_i16 / v_pk_max_i16): the three taps of a row are the dwords
+// (p[x-1], p[x]), (p[x], p[x+1]), (p[x+1], p[x+2]) made by v_alignbit from the
+// aligned words at x - 2, x, x + 2 (replicate border).  Needs an even width,
+// even strides and 4-byte-aligned rows (median3x3_device checks).
+__device__ __forceinline__ void sort2p(uint32_t& a, uint32_t& b)
+{
+    const uint32_t lo = pk_min(a, b), hi = as_u(__builtin_elementwise_max(as_s2(a), as_s2(b)));
+    a = lo;
+    b = hi;
+}
+
+__global__ __launch_bounds__(256) void median3x3_pk_kernel(const int16_t* __restrict__ src, size_t ss,
+                                                           size_t sfs, int16_t* __restrict__ dst,
+                                                           size_t ds, size_t dfs, int W, int H,
+                                                           const int* __restrict__ poison,
+                                                           unsigned epoch, int invalid)
+{
+    const int i = blockIdx.x * 64 + (threadIdx.x & 63);  // pixel pair (2i, 2i + 1)
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.z;
+    if (2 * i >= W || y >= H) return;
+    uint32_t* o = (uint32_t*)(dst + f * dfs + (size_t)y * ds) + i;
+    if (poison && __builtin_expect(*poison == (int)epoch, 0)) {
+        *o = (uint32_t)(invalid & 0xffff) * 0x10001u;
+        return;
+    }
+    const int16_t* s = src + f * sfs;
+    uint32_t t[9];
+    const int rows[3] = {max(y - 1, 0), y, min(y + 1, H - 1)};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint32_t* q = (const uint32_t*)(s + (size_t)rows[k] * ss);
+        const uint32_t M = q[i];
+        const uint32_t P = i > 0 ? q[i - 1] : M << 16;             // hi half = p[x - 1] (p[0] at x = 0)
+        const uint32_t N = 2 * i + 2 < W ? q[i + 1] : M >> 16;     // lo half = p[x + 2] (p[W - 1] at the end)
+        t[3 * k] = __builtin_amdgcn_alignbit(M, P, 16);
+        t[3 * k + 1] = M;
+        t[3 * k + 2] = __builtin_amdgcn_alignbit(N, M, 16);
+    }
+    // the 19-exchange network of med9 on both pixels at once
+    sort2p(t[1], t[2]); sort2p(t[4], t[5]); sort2p(t[7], t[8]);
+    sort2p(t[0], t[1]); sort2p(t[3], t[4]); sort2p(t[6], t[7]);
+    sort2p(t[1], t[2]); sort2p(t[4], t[5]); sort2p(t[7], t[8]);
+    sort2p(t[0], t[3]); sort2p(t[5], t[8]); sort2p(t[4], t[7]);
+    sort2p(t[3], t[6]); sort2p(t[1], t[4]); sort2p(t[2], t[5]);
+    sort2p(t[4], t[7]); sort2p(t[4], t[2]); sort2p(t[6], t[4]);
+    sort2p(t[4], t[2]);
+    *o = t[4];
+}
+
 // ---- speckle filter: union-find ----------------------------------------------
 // Stage 1: union-find inside a 32x32 tile in LDS (one 256-thread block per
-// tile, 4 pixels per thread).  Every valid pixel's global parent = its
-// tile-local root (row-major local order is monotone in the global index, so
-// roots stay the smallest index of their tile component); tile[root] = the
-// tile component's pixel count, tile[other] = 0; size[root] = 0.
+// tile, 4 pixels per thread).  Outputs: per pixel its tile-local root (u16, lroot; row-major
+// local order is monotone in the global index, so a root is the smallest
+// global index of its tile component); per tile component (at its root's
+// global index gi): parent[gi] = gi, tilew[gi] = the component's pixel count,
+// size[gi] = 0, and gi + frame * W * H appended to the compact root list.
 constexpr int kSpTile = 32;
 
 __device__ __forceinline__ int lds_load(const int* p)
@@ -105,12 +158,13 @@ __device__ void lunite(int* par, int a, int b)
     }
 }
 
-__global__ __launch_bounds__(256) void speckle_local_kernel(const int16_t* __restrict__ img,
-                                                            size_t st, size_t fs, int W, int H,
-                                                            int new_val, int max_diff,
+__global__ __launch_bounds__(256) void speckle_local_kernel(int16_t* __restrict__ img, size_t st, size_t fs,
+                                                            int W, int H, int new_val, int max_diff,
                                                             int* __restrict__ parent,
-                                                            int* __restrict__ tile,
-                                                            int* __restrict__ size)
+                                                            int* __restrict__ tilew,
+                                                            int* __restrict__ size,
+                                                            uint16_t* __restrict__ lroot,
+                                                            unsigned* __restrict__ list)
 {
     __shared__ int lpar[kSpTile * kSpTile];
     __shared__ int lval[kSpTile * kSpTile];
@@ -119,8 +173,8 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(const int16_t* __res
     const int lane = threadIdx.x & 63;
     const int x0 = blockIdx.x * kSpTile, y0 = blockIdx.y * kSpTile;
     const int f = blockIdx.z;
-    const int16_t* s = img + f * fs;
     const int kInvalid = 0x7fffffff;
+    const int16_t* s = img + f * fs;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int ly = ty + 8 * k, li = ly * kSpTile + tx;
@@ -185,20 +239,35 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(const int16_t* __res
         }
     }
     __syncthreads();
-    int* par = parent + (size_t)f * W * H;
-    int* tl = tile + (size_t)f * W * H;
-    int* sz = size + (size_t)f * W * H;
+    const size_t npix = (size_t)W * H;
+    int* par = parent + f * npix;
+    int* tl = tilew + f * npix;
+    int* sz = size + f * npix;
+    uint16_t* lr = lroot + f * npix;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int ly = ty + 8 * k, li = ly * kSpTile + tx;
         const int gx = x0 + tx, gy = y0 + ly;
-        if (gx >= W || gy >= H) continue;
+        const bool in = gx < W && gy < H;
         const int gi = gy * W + gx;
-        const int r = root[k];
-        par[gi] = r >= 0 ? (y0 + r / kSpTile) * W + x0 + (r % kSpTile) : gi;
+        if (in) lr[gi] = (uint16_t)(root[k] >= 0 ? root[k] : 0xffff);
         const int c = lcnt[li];
-        tl[gi] = c;
-        if (c > 0) sz[gi] = 0;
+        const bool isroot = in && c > 0;
+        if (isroot) {
+            par[gi] = gi;
+            tl[gi] = c;
+            sz[gi] = 0;
+        }
+        // wave-aggregated append to the compact root list (list[0] = count)
+        const unsigned long long m = __ballot(isroot);
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            unsigned base = 0;
+            if (lane == leader) base = atomicAdd(list, (unsigned)__popcll(m));
+            base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
+            if (isroot)
+                list[1 + base + (unsigned)__popcll(m & ((1ull << lane) - 1ull))] = (unsigned)(f * npix + gi);
+        }
     }
 }
 
@@ -242,18 +311,30 @@ __device__ void uf_unite(int* parent, int a, int b)
     }
 }
 
-// Stage 2: unions across tile borders (right and bottom edge of each tile),
-// one wave per tile.  A pair joins the two pixels' tile components; lanes
-// whose (component, component) pair repeats a lower lane's skip it, so a
-// tile edge inside one smooth region costs one union instead of 32.
-__global__ __launch_bounds__(64) void speckle_border_kernel(const int16_t* __restrict__ img,
-                                                            size_t st, size_t fs, int W, int H,
-                                                            int new_val, int max_diff,
-                                                            int* __restrict__ parent)
+// the tile root (global index) of pixel (x, y) from its local root
+__device__ __forceinline__ int tile_root(const uint16_t* lr, int W, int x, int y)
 {
-    const int t = threadIdx.x;
-    const int x0 = blockIdx.x * kSpTile, y0 = blockIdx.y * kSpTile;
-    const int f = blockIdx.z;
+    const int l = lr[y * W + x];
+    return (y & ~(kSpTile - 1)) * W + (x & ~(kSpTile - 1)) + (l / kSpTile) * W + (l % kSpTile);
+}
+
+// Stage 2: unions across tile borders (right and bottom edge of each tile),
+// one wave per tile, four tiles per block.  A pair joins the two pixels' tile
+// components; lanes whose (component, component) pair repeats a lower lane's
+// skip it, so a tile edge inside one smooth region costs one union instead of
+// 32.
+__global__ __launch_bounds__(256) void speckle_border_kernel(const int16_t* __restrict__ img,
+                                                             size_t st, size_t fs, int W, int H,
+                                                             int new_val, int max_diff,
+                                                             int* __restrict__ parent,
+                                                             const uint16_t* __restrict__ lroot,
+                                                             int tiles_x)
+{
+    const int t = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int tyi = tile / tiles_x;
+    const int x0 = (tile - tyi * tiles_x) * kSpTile, y0 = tyi * kSpTile;
+    const int f = blockIdx.y;
     int x, y, nx, ny;
     if (t < kSpTile) {  // right edge: (x0+31, y0+t) -- (x0+32, y0+t)
         x = x0 + kSpTile - 1;
@@ -266,14 +347,16 @@ __global__ __launch_bounds__(64) void speckle_border_kernel(const int16_t* __res
         nx = x;
         ny = y + 1;
     }
-    int* par = parent + (size_t)f * W * H;
+    const size_t npix = (size_t)W * H;
+    int* par = parent + f * npix;
+    const uint16_t* lr = lroot + f * npix;
     int a = -1, b = -1;
-    if (x < W && y < H && nx < W && ny < H) {
+    if (y0 < H && x < W && y < H && nx < W && ny < H) {
         const int16_t* s = img + f * fs;
         const int v = s[(size_t)y * st + x], u = s[(size_t)ny * st + nx];
         if (v != new_val && u != new_val && abs(v - u) <= max_diff) {
-            a = par[y * W + x];  // tile roots (written by stage 1)
-            b = par[ny * W + nx];
+            a = tile_root(lr, W, x, y);
+            b = tile_root(lr, W, nx, ny);
         }
     }
     bool pending = a >= 0;
@@ -288,43 +371,46 @@ __global__ __launch_bounds__(64) void speckle_border_kernel(const int16_t* __res
     }
 }
 
-// Stage 3: per tile component: its global root, the component sizes, and the
-// tile word becomes ~root (negative: "resolved").
+// Stage 3: per tile component (the compact root list, grid-stride): its
+// global root, the component sizes, and the tile word becomes ~root
+// (negative: "resolved").
 __global__ __launch_bounds__(256) void speckle_count_kernel(int W, int H, int* __restrict__ parent,
-                                                            int* __restrict__ tile,
-                                                            int* __restrict__ size)
+                                                            int* __restrict__ tilew,
+                                                            int* __restrict__ size,
+                                                            const unsigned* __restrict__ list)
 {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const int f = blockIdx.y;
-    if (i >= W * H) return;
-    int* tl = tile + (size_t)f * W * H;
-    const int c = tl[i];
-    if (c <= 0) return;
-    int* par = parent + (size_t)f * W * H;
-    const int g = uf_find(par, i);
-    atomicAdd(size + (size_t)f * W * H + g, c);
-    tl[i] = ~g;
+    const unsigned cnt = list[0];
+    const size_t npix = (size_t)W * H;
+    for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256) {
+        const unsigned e = list[1 + i];
+        const size_t f = e / npix;
+        const int gi = (int)(e - f * npix);
+        int* par = parent + f * npix;
+        const int g = uf_find(par, gi);
+        atomicAdd(size + f * npix + g, tilew[f * npix + gi]);
+        tilew[f * npix + gi] = ~g;
+    }
 }
 
-// Stage 4: pixel -> tile root -> global root -> size.
+// Stage 4: pixel -> tile root -> global root -> size.  Block (0, 0, 0) also
+// rewinds the root list for the next call (stage 3 has finished with it).
 __global__ __launch_bounds__(256) void speckle_apply_kernel(int16_t* __restrict__ img, size_t st,
                                                             size_t fs, int W, int H, int new_val,
                                                             int max_size,
-                                                            const int* __restrict__ parent,
-                                                            const int* __restrict__ tile,
-                                                            const int* __restrict__ size)
+                                                            const int* __restrict__ tilew,
+                                                            const int* __restrict__ size,
+                                                            const uint16_t* __restrict__ lroot,
+                                                            unsigned* __restrict__ list)
 {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
     const int f = blockIdx.z;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && f == 0 && threadIdx.x == 0) list[0] = 0u;
     if (x >= W || y >= H) return;
     int16_t* p = img + f * fs + (size_t)y * st + x;
     if (*p == new_val) return;
     const size_t base = (size_t)f * W * H;
-    const int i = y * W + x;
-    int t = tile[base + i];
-    if (t >= 0) t = tile[base + parent[base + i]];  // not a tile root: its root's word
-    const int g = ~t;
+    const int g = ~tilew[base + tile_root(lroot + base, W, x, y)];
     if (size[base + g] <= max_size) *p = (int16_t)new_val;
 }
 
@@ -518,36 +604,77 @@ int median3x3_device(mvsv_ctx* ctx, int n, const int16_t* src, size_t ss, size_t
                      size_t ds, size_t dfs, int W, int H, const int* poison, unsigned epoch,
                      int invalid)
 {
-    dim3 grid((W + 63) / 64, (H + 3) / 4, n);
-    hipLaunchKernelGGL(median3x3_kernel, grid, dim3(256), 0, ctx->stream, src, ss, sfs, dst, ds,
-                       dfs, W, H, poison, epoch, invalid);
+    const bool packed = (W % 2) == 0 && (ss % 2) == 0 && (sfs % 2) == 0 && (ds % 2) == 0 && (dfs % 2) == 0 &&
+                        ((uintptr_t)src & 3) == 0 && ((uintptr_t)dst & 3) == 0;
+    if (packed) {
+        dim3 grid((W / 2 + 63) / 64, (H + 3) / 4, n);
+        hipLaunchKernelGGL(median3x3_pk_kernel, grid, dim3(256), 0, ctx->stream, src, ss, sfs, dst, ds, dfs, W, H,
+                           poison, epoch, invalid);
+    } else {
+        dim3 grid((W + 63) / 64, (H + 3) / 4, n);
+        hipLaunchKernelGGL(median3x3_kernel, grid, dim3(256), 0, ctx->stream, src, ss, sfs, dst, ds, dfs, W, H,
+                           poison, epoch, invalid);
+    }
     return check_hip(ctx, hipGetLastError(), "median3x3");
+}
+
+// The speckle filter's buffers: parent / tile words / sizes (int per pixel,
+// only tile-component roots used), the tile-local root of every pixel (u16)
+// and the compact root list (count + entries).
+static int speckle_buffers(mvsv_ctx* ctx, int n, int W, int H, int** parent, int** tilew, int** size,
+                           uint16_t** lroot, unsigned** list)
+{
+    int rc;
+    const size_t npix = (size_t)n * W * H;
+    // the list count is rewound by the apply kernel of every run; a fresh
+    // (re)allocation, or a run that did not reach its apply launch, rewinds here
+    const bool fresh_list = ctx->uf_list.bytes < (npix + 1) * 4 || ctx->uf_list_dirty;
+    if ((rc = ensure(ctx, ctx->uf_parent, npix * 4, "speckle labels"))) return rc;
+    if ((rc = ensure(ctx, ctx->uf_size, npix * 4, "speckle sizes"))) return rc;
+    if ((rc = ensure(ctx, ctx->uf_tile, npix * 4, "speckle tile components"))) return rc;
+    if ((rc = ensure(ctx, ctx->uf_lroot, npix * 2, "speckle local roots"))) return rc;
+    if ((rc = ensure(ctx, ctx->uf_list, (npix + 1) * 4, "speckle root list"))) return rc;
+    if (fresh_list && (rc = check_hip(ctx, hipMemsetAsync(ctx->uf_list.ptr, 0, 4, ctx->stream), "root list reset")))
+        return rc;
+    ctx->uf_list_dirty = true;  // until this run's apply kernel is launched
+    *parent = (int*)ctx->uf_parent.ptr;
+    *size = (int*)ctx->uf_size.ptr;
+    *tilew = (int*)ctx->uf_tile.ptr;
+    *lroot = (uint16_t*)ctx->uf_lroot.ptr;
+    *list = (unsigned*)ctx->uf_list.ptr;
+    return MVSV_OK;
+}
+
+// stages 2-4 (stage 1 launched by the caller)
+static int speckle_tail(mvsv_ctx* ctx, int n, int16_t* img, size_t st, size_t fs, int W, int H, int new_val,
+                        int max_size, int max_diff, int* parent, int* tilew, int* size, uint16_t* lroot,
+                        unsigned* list)
+{
+    hipStream_t s = ctx->stream;
+    const int tx = (W + kSpTile - 1) / kSpTile, tyn = (H + kSpTile - 1) / kSpTile;
+    hipLaunchKernelGGL(speckle_border_kernel, dim3((unsigned)((tx * tyn + 3) / 4), n), dim3(256), 0, s, img, st, fs,
+                       W, H, new_val, max_diff, parent, lroot, tx);
+    hipLaunchKernelGGL(speckle_count_kernel, dim3((unsigned)std::max(1, ctx->cus * 4)), dim3(256), 0, s, W, H, parent,
+                       tilew, size, list);
+    dim3 grid((W + 63) / 64, (H + 3) / 4, n);
+    hipLaunchKernelGGL(speckle_apply_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val, max_size, tilew,
+                       size, lroot, list);
+    const int rc = check_hip(ctx, hipGetLastError(), "speckle filter");
+    if (rc == MVSV_OK) ctx->uf_list_dirty = false;
+    return rc;
 }
 
 int speckle_device(mvsv_ctx* ctx, int n, int16_t* img, size_t st, size_t fs, int W, int H,
                    int new_val, int max_size, int max_diff)
 {
-    int rc;
-    const size_t npix = (size_t)W * H;
-    if ((rc = ensure(ctx, ctx->uf_parent, (size_t)n * npix * 4, "speckle labels"))) return rc;
-    if ((rc = ensure(ctx, ctx->uf_size, (size_t)n * npix * 4, "speckle sizes"))) return rc;
-    if ((rc = ensure(ctx, ctx->uf_tile, (size_t)n * npix * 4, "speckle tile components")))
-        return rc;
-    int* parent = (int*)ctx->uf_parent.ptr;
-    int* size = (int*)ctx->uf_size.ptr;
-    int* tile = (int*)ctx->uf_tile.ptr;
-    hipStream_t s = ctx->stream;
+    int rc, *parent, *tilew, *size;
+    uint16_t* lroot;
+    unsigned* list;
+    if ((rc = speckle_buffers(ctx, n, W, H, &parent, &tilew, &size, &lroot, &list))) return rc;
     dim3 tiles((W + kSpTile - 1) / kSpTile, (H + kSpTile - 1) / kSpTile, n);
-    hipLaunchKernelGGL(speckle_local_kernel, tiles, dim3(256), 0, s, img, st, fs, W, H, new_val,
-                       max_diff, parent, tile, size);
-    hipLaunchKernelGGL(speckle_border_kernel, tiles, dim3(64), 0, s, img, st, fs, W, H, new_val,
-                       max_diff, parent);
-    hipLaunchKernelGGL(speckle_count_kernel, dim3((unsigned)((npix + 255) / 256), n), dim3(256), 0,
-                       s, W, H, parent, tile, size);
-    dim3 grid((W + 63) / 64, (H + 3) / 4, n);
-    hipLaunchKernelGGL(speckle_apply_kernel, grid, dim3(256), 0, s, img, st, fs, W, H, new_val,
-                       max_size, parent, tile, size);
-    return check_hip(ctx, hipGetLastError(), "speckle filter");
+    hipLaunchKernelGGL(speckle_local_kernel, tiles, dim3(256), 0, ctx->stream, img, st, fs, W, H, new_val, max_diff,
+                       parent, tilew, size, lroot, list);
+    return speckle_tail(ctx, n, img, st, fs, W, H, new_val, max_size, max_diff, parent, tilew, size, lroot, list);
 }
 
 int mean_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st, size_t fs, int W, int H,

@@ -608,19 +608,28 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                     ring[s][i] = h;
                     const bool pin = pin_row || (i == 0 && pin_x0);
                     ov[i] = pin ? p2x2 : pk_add_u16(p2x2, csum[i]);
-                    if (emit && i < nout) orow[i * PP] = ov[i];
+                }
+                // every column of the wave inside the image (all but the last
+                // tile column): unpredicated stores
+                const bool full = __all(nout == kCost2Run);
+                if (emit) {
+#pragma unroll
+                    for (int i = 0; i < kCost2Run; i++)
+                        if (full || i < nout) orow[i * PP] = ov[i];
                 }
                 // residual plane + per-pixel minimum: the lanes of a column
                 // lane hold its pixel's D costs (PP <= 64 lanes, an aligned
-                // segment of the wave).  The four columns' minima: pairs
-                // (m0, m1) and (m2, m3) per lane, then one transposing step
-                // (even lanes keep reducing (m0, m1), odd lanes (m2, m3)) and
-                // five parity-preserving butterfly steps on a single dword.
+                // segment of the wave).  Columns are paired (0, 1), (2, 3):
+                // Plo = (c0[2p], c1[2p]), Phi = (c0[2p+1], c1[2p+1]); their
+                // minima per lane, then one transposing step (even lanes keep
+                // reducing columns (0, 1), odd lanes (2, 3)) and five
+                // parity-preserving butterfly steps on a single dword.
                 if (Rv && emit) {
-                    uint32_t A = pk_min_u16(__builtin_amdgcn_perm(ov[1], ov[0], 0x05040100u),
-                                            __builtin_amdgcn_perm(ov[1], ov[0], 0x07060302u));
-                    uint32_t B = pk_min_u16(__builtin_amdgcn_perm(ov[3], ov[2], 0x05040100u),
-                                            __builtin_amdgcn_perm(ov[3], ov[2], 0x07060302u));
+                    const uint32_t Plo01 = __builtin_amdgcn_perm(ov[1], ov[0], 0x05040100u);
+                    const uint32_t Phi01 = __builtin_amdgcn_perm(ov[1], ov[0], 0x07060302u);
+                    const uint32_t Plo23 = __builtin_amdgcn_perm(ov[3], ov[2], 0x05040100u);
+                    const uint32_t Phi23 = __builtin_amdgcn_perm(ov[3], ov[2], 0x07060302u);
+                    uint32_t A = pk_min_u16(Plo01, Phi01), B = pk_min_u16(Plo23, Phi23);
                     const bool odd = (p & 1) != 0;
                     uint32_t X = pk_min_u16(odd ? B : A,
                                             (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? A : B), 0xB1, 0xf, 0xf, false));
@@ -638,30 +647,26 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                     const uint32_t Y = (uint32_t)__builtin_amdgcn_mov_dpp((int)X, 0xB1, 0xf, 0xf, false);
                     A = odd ? Y : X;  // (m0, m1) in every lane
                     B = odd ? X : Y;  // (m2, m3)
-                    // per-pixel minimum (the final kernel's absolute cost base)
-                    if (p == 0) {
-                        uint16_t* mrow = Mv + (size_t)(orow - (uint32_t*)C) / PP;
-                        const uint32_t mv[kCost2Run] = {A, A >> 16, B, B >> 16};
-#pragma unroll
-                        for (int i = 0; i < kCost2Run; i++)
-                            if (i < nout) mrow[i] = (uint16_t)mv[i];
+                    // per-pixel minimum (the final kernel's absolute cost base):
+                    // lane p < 4 stores column p's
+                    if (p < kCost2Run && p < nout) {
+                        const uint32_t ab = p < 2 ? A : B;
+                        Mv[(size_t)(orow - (uint32_t*)C) / PP + p] = (uint16_t)(p & 1 ? ab >> 16 : ab);
                     }
-                    // R = min(C - m, 2 P2) + P2 = min(C - (m - P2), 3 P2), byte
-                    // = R(2p) + 16 R(2p + 1) (one v_dot2_u32_u16)
-                    const uint32_t Am = pk_sub_u16(A, p2x2), Bm = pk_sub_u16(B, p2x2);
-                    const uint32_t mm[kCost2Run] = {
-                        __builtin_amdgcn_perm(Am, Am, 0x01000100u), __builtin_amdgcn_perm(Am, Am, 0x03020302u),
-                        __builtin_amdgcn_perm(Bm, Bm, 0x01000100u), __builtin_amdgcn_perm(Bm, Bm, 0x03020302u)};
-                    uint8_t* rrow = Rv + (orow - (uint32_t*)C);  // byte (pixel, pair) = dword (pixel, pair) of C
+                    // R = min(C - m, 2 P2) + P2 = min(C - (m - P2), 3 P2) on the
+                    // column pairs; one word holds columns 0 and 1's residual
+                    // bytes R[2p] | R[2p+1] << 4 in bits 0-7 and 16-23
                     const uint32_t p2x3 = pk_add_u16(pk_add_u16(p2x2, p2x2), p2x2);
-                    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-                    const u16x2 nib = {1, 16};
+                    const uint32_t Am = pk_sub_u16(A, p2x2), Bm = pk_sub_u16(B, p2x2);
+                    const uint32_t r01 = pk_min_u16(pk_sub_u16(Plo01, Am), p2x3) |
+                                         (pk_min_u16(pk_sub_u16(Phi01, Am), p2x3) << 4);
+                    const uint32_t r23 = pk_min_u16(pk_sub_u16(Plo23, Bm), p2x3) |
+                                         (pk_min_u16(pk_sub_u16(Phi23, Bm), p2x3) << 4);
+                    uint8_t* rrow = Rv + (orow - (uint32_t*)C);  // byte (pixel, pair) = dword (pixel, pair) of C
+                    const uint32_t rw[kCost2Run] = {r01, r01 >> 16, r23, r23 >> 16};
 #pragma unroll
-                    for (int i = 0; i < kCost2Run; i++) {
-                        const uint32_t r = pk_min_u16(pk_sub_u16(ov[i], mm[i]), p2x3);
-                        if (i < nout)
-                            rrow[i * PP] = (uint8_t)__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, r), nib, 0u, false);
-                    }
+                    for (int i = 0; i < kCost2Run; i++)
+                        if (full || i < nout) rrow[i * PP] = (uint8_t)rw[i];
                 }
             }
         }
@@ -1457,7 +1462,9 @@ struct TriCfg {
     static constexpr int kSW = kCPW * kWaves;  // U-columns per strip
     static constexpr int kThreads = 64 * (kWaves + 1);
     // blocks per CU the register budget aims at: one 1024-thread block, or two
-    // 512-thread ones (4 waves per SIMD either way); D = 256 on 16 lanes: 2
+    // 512-thread ones (4 waves per SIMD either way); D = 256 on 16 lanes: 2.
+    // (Narrow strips reading the cost residual aim at 5: two 9-wave blocks
+    // per CU, each filling the other's step-barrier and hand-off waits.)
     static constexpr int kWavesPerEU = (NP >= 8 && LPC == 16) ? 2 : 4;
 };
 #ifndef MVSV_TRI_PF
@@ -1544,7 +1551,7 @@ __device__ __forceinline__ size_t tri_slot(int chain, int k, int t, int nchains,
 
 template <int NP, int WV, int LPC, typename AccT, bool NW = false, bool RES = false>
 __global__ __launch_bounds__((TriCfg<NP, WV, LPC>::kThreads))
-__attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU))) void sgbm_tri_kernel(
+__attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU + (RES && WV <= 8 && NP <= 4 ? 1 : 0)))) void sgbm_tri_kernel(
     const void* __restrict__ C, AccT* __restrict__ A, size_t plane, AccT* __restrict__ dummy,
     int H, int W1, int D, int npass, int P1, int P2, unsigned long long* __restrict__ bnd,
     unsigned epoch, int nframes, int nstrips, int* __restrict__ status, unsigned spin_limit,
@@ -2351,7 +2358,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     // the pending flush's first step and count, wave-uniform).
     struct Pend {
         uint2 rec;
-        int mC, cm, cp;
+        int mC;
+        uint2 cw;  // C[base .. base + 3] of the column, base = min((best - 1) & ~1, D - 4)
     } pend{};
     int pend_s0 = 0, pend_cnt = 0;
     const int16_t* crow = C + f * frame + (size_t)y * W1 * D;
@@ -2372,9 +2380,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
             const int c1 = Spp >= clampS ? cv - q.mC : 0;
             return min(base + Spp + ndir * (c1 - min(c1, 2 * e.P2)), kMaxCost);
         };
-        const int Sm = exact((int)(q.rec.y & 0xffffu), q.cm), Sp = exact((int)(q.rec.y >> 16), q.cp);
-        finish(exists && rl < cnt, W1 - 1 - (s0 + rl), rec_best(kK), min(base + (int)(kK >> 16), kMaxCost),
-               Sm, Sp, 0);
+        const int best = rec_best(kK);
+        const int bm = max(best - 1, 0), bp = min(best + 1, D - 1);
+        const int cb0 = min(bm & ~1, D - 4);
+        auto cword = [&](int d) -> int {  // C(d) out of the loaded 4-element window
+            const int i = d - cb0;
+            const uint32_t w = (i & 2) ? q.cw.y : q.cw.x;
+            return (int)((i & 1) ? (w >> 16) : (w & 0xffffu));
+        };
+        const int Sm = exact((int)(q.rec.y & 0xffffu), cword(bm)), Sp = exact((int)(q.rec.y >> 16), cword(bp));
+        finish(exists && rl < cnt, W1 - 1 - (s0 + rl), best, min(base + (int)(kK >> 16), kMaxCost), Sm, Sp, 0);
     };
     auto flush_res = [&](int s0, int cnt) {
         Pend q;
@@ -2383,10 +2398,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
         const int best = rec_best(q.rec.x & 0x7fffffffu);
         const int xc = own ? W1 - 1 - (s0 + rl) : 0;
         q.mC = mrowp[xc];
-        const int bm = max(best - 1, 0), bp = min(best + 1, D - 1);
-        // one shared address for the lanes that need no exact cost
-        q.cm = crow[(own && (int)(q.rec.y & 0xffffu) >= clampS) ? (size_t)xc * D + bm : 0];
-        q.cp = crow[(own && (int)(q.rec.y >> 16) >= clampS) ? (size_t)xc * D + bp : 0];
+        // C(best - 1) and C(best + 1) in one 8-byte load (4-byte aligned, inside
+        // the pixel's D costs); one shared address for the lanes that need no
+        // exact cost
+        const int cb0 = min(max(best - 1, 0) & ~1, D - 4);
+        const bool need = own && ((int)(q.rec.y & 0xffffu) >= clampS || (int)(q.rec.y >> 16) >= clampS);
+        q.cw = *(const uint2*)(crow + (need ? (size_t)xc * D + cb0 : 0));
         finish_res(pend, pend_s0, pend_cnt);  // the previous flush's columns (none the first time)
         pend = q;
         pend_s0 = s0;
@@ -2868,11 +2885,16 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
         // 256 -- and the L->R lines fill idle ones); after them for batches,
         // where both kernels saturate the GPU and running them together was
         // measured slower
+        // Round 4: with the residual input the line kernel needs 53 VGPRs and
+        // the wide strip kernel 103, so a line wave fits beside a strip block
+        // on every SIMD -- launched after the strips on the second stream, the
+        // lines fill the strips' step-barrier and hand-off waits (one batch of
+        // 8 frames: 4.49 -> 4.37-4.40 ms, MI355X r04d A/B)
         int aux_mode = ctx->lines_aux;
         if (aux_mode < 0) {
             constexpr int wide = tri_wide_waves<NP>();
             const long long blocks = (long long)npass * n * ((e.W1 + H - 1 + 4 * wide - 1) / (4 * wide));
-            aux_mode = blocks < ctx->cus ? 1 : 0;
+            aux_mode = blocks < ctx->cus ? 1 : (RES ? 2 : 0);
         }
         hipStream_t ls = aux_mode ? ctx->aux : s;
         auto lines = [&]() {
@@ -3251,13 +3273,11 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     // a strip launch of this call that gave up a wait poisons the median's output
     const bool strips_ran = ctx->tri_epoch != epoch0;
     StageTimer tm(ctx, kStagePost);
-    if ((rc = median3x3_device(ctx, n, raw, W, plane, out, os, ofs, W, H,
-                               strips_ran ? (const int*)ctx->status.ptr : nullptr, ctx->tri_epoch,
-                               e.invalid)))
+    const int* poison = strips_ran ? (const int*)ctx->status.ptr : nullptr;
+    if ((rc = median3x3_device(ctx, n, raw, W, plane, out, os, ofs, W, H, poison, ctx->tri_epoch, e.invalid)))
         return rc;
     if (e.speckle_window > 0)
-        return speckle_device(ctx, n, out, os, ofs, W, H, e.invalid, e.speckle_window,
-                              e.speckle_diff);
+        return speckle_device(ctx, n, out, os, ofs, W, H, e.invalid, e.speckle_window, e.speckle_diff);
     return MVSV_OK;
 }
 

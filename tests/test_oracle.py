@@ -203,3 +203,43 @@ def test_oracle_resize_linear_properties(oracle):
         ref = (A[y0][:, x0] * (1 - ax) + A[y0][:, x1] * ax) * (1 - ay) + \
               (A[y1][:, x0] * (1 - ax) + A[y1][:, x1] * ax) * ay
         assert np.abs(r - ref).max() <= 1.0, f
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_cost_residual_invariance(seed):
+    """The cost residual plane (mvsv.h MVSV_OPT_COST_RESIDUAL) on the numpy twin:
+    with R = min(C - min_d C, 2*P2) + P2 every direction's path deltas
+    L_r - (C - P2) equal those computed from C, and the aggregated
+    S'' = n*(R - P2) + deltas has the argmin (first minimum) of S and the same
+    minimum up to n*(min_d C - P2) -- the identity the direction kernels and
+    the residual final kernel rely on (no-wrap regime, 3*P2 <= 15)."""
+    from oracle import twin
+    rng = np.random.default_rng(700 + seed)
+    H, W, D = 24, 70, 16
+    L = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    L[:, 20:30] = 90  # flat patch: ties and equal costs
+    R = np.roll(L, -3, axis=1).astype(int) + rng.integers(-2, 3, (H, W))
+    R = np.clip(R, 0, 255).astype(np.uint8)
+    p = dict(min_disparity=0, num_disparities=D, block_size=3, p1=2, p2=5, disp12_max_diff=1,
+             pre_filter_cap=0, uniqueness_ratio=0, speckle_window_size=0, speckle_range=0,
+             mode=seed % 2)
+    e = twin.sgbm_effective(p, W)
+    P1, P2 = e["P1"], e["P2"]
+    C = twin.sgbm_cost_volume(L, R, p).astype(np.int32)
+    m = C.min(axis=-1, keepdims=True)
+    Rr = np.minimum(C - m, 2 * P2) + P2
+    Ssum = np.zeros_like(C)
+    Spp = np.zeros_like(C)
+    dirs = twin.sgbm_directions(p["mode"])
+    for dx, dy in dirs:
+        dC = twin.sgbm_path(C, dx, dy, P1, P2) - (C - P2)
+        dR = twin.sgbm_path(Rr, dx, dy, P1, P2) - (Rr - P2)
+        assert np.array_equal(dC, dR), (dx, dy)
+        assert dC.min() >= 0 and dC.max() <= P2
+        Ssum += dC
+        Spp += dR
+    n = len(dirs)
+    S = n * (C - P2) + Ssum       # no saturation at these sizes
+    S2 = n * (Rr - P2) + Spp
+    assert np.array_equal(S.argmin(axis=-1), S2.argmin(axis=-1))
+    assert np.array_equal(S.min(axis=-1), S2.min(axis=-1) + n * (m[..., 0] - P2))
