@@ -43,6 +43,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "--one":  # --one NAME N: one case (coun
     run("one", cases=case, batches=(int(sys.argv[3]),))
     sys.exit(0)
 run("auto")
+if len(sys.argv) > 1 and sys.argv[1] == "--auto":  # the chosen tile height only (A/B runs)
+    sys.exit(0)
 for ty in (8, 12, 16, 20):
     os.environ["MVSV_BM_TY"] = str(ty)
     run(f"ty={ty}", batches=(8,))

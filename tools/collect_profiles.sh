@@ -1,13 +1,13 @@
 #!/bin/bash
 # Copy the summaries of one tools/gpu_round.sh session (gpurun_out/TAG) into
-# profiles/r03/TAG (tracked) and refresh the top-level counter summaries that
-# bench.py reads (profiles/r03/{sq_summary,pmc_traffic}.json).
+# profiles/r04/TAG (tracked) and refresh the top-level counter summaries that
+# bench.py reads (profiles/r04/{sq_summary,pmc_traffic}.json).
 # Usage (here, after the gpurun call): bash tools/collect_profiles.sh TAG
 set -e
 T=$1
 R=$(cd "$(dirname "$0")/.." && pwd)
 S=$R/gpurun_out/$T
-D=$R/profiles/r03/$T
+D=$R/profiles/r04/$T
 mkdir -p $D
 cp $S/bench.json $S/configs.jsonl $S/stream_config5.json $S/valu_rate.txt $S/sq_summary.txt \
    $S/sq_summary.json $S/pmc_traffic.json $D/
@@ -21,5 +21,5 @@ cp $(find $S/pmc_write -name '*counter_collection.csv' | head -1) $D/pmc_write_c
 cp $(find $S/sq/p1 -name '*counter_collection.csv' | head -1) $D/sq_p1_counter_collection.csv
 cp $(find $S/sq/p2 -name '*counter_collection.csv' | head -1) $D/sq_p2_counter_collection.csv
 cp $(find $S/ubench_pmc -name '*counter_collection.csv' | head -1) $D/ubench_pmc_counter_collection.csv
-cp $D/sq_summary.json $D/pmc_traffic.json $R/profiles/r03/
-echo "profiles/r03/$T:"; ls $D
+cp $D/sq_summary.json $D/pmc_traffic.json $R/profiles/r04/
+echo "profiles/r04/$T:"; ls $D

@@ -10,7 +10,7 @@ set -o pipefail
 TAG=${1:-run}
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
-P=$R/profiles/r03
+P=$R/profiles/r04
 mkdir -p $O $P
 export TMPDIR=/tmp
 cd $R
@@ -27,8 +27,8 @@ cd $R
 bash tools/sq_counters.sh $TAG/sq || exit 1
 python tools/sq_summary.py $O/sq $WL $O/sq_summary.json > $O/sq_summary.txt && cp $O/sq_summary.json $P/sq_summary.json || { echo "sq summary failed"; exit 1; }
 cd /tmp
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 2 --warmup 1 --inflight 1 --profile-steps 2 > $O/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
-timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 2 --warmup 1 --inflight 1 --profile-steps 2 > $O/pmc_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 2 --warmup 1 --inflight 1 --profile-steps 2 --no-configs > $O/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 2 --warmup 1 --inflight 1 --profile-steps 2 --no-configs > $O/pmc_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
 cd $R
 python tools/pmc_traffic.py $(find $O/pmc_fetch -name '*counter_collection.csv' | head -1) $(find $O/pmc_write -name '*counter_collection.csv' | head -1) $WL $O/pmc_traffic.json > /dev/null && cp $O/pmc_traffic.json $P/pmc_traffic.json || { echo "pmc summary failed"; exit 1; }
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
@@ -38,8 +38,8 @@ timeout -k 10 600 python tools/bench_configs.py > $O/configs.jsonl 2> $O/configs
 timeout -k 10 300 python tools/bench_stream.py > $O/stream_config5.json 2> $O/stream.err || { echo "stream bench failed"; exit 1; }
 timeout -k 10 120 python tools/c5_frame.py > $O/c5_frame.jsonl 2>/dev/null && timeout -k 10 120 python tools/c5_frame.py --frames 2 >> $O/c5_frame.jsonl 2>/dev/null || { echo "config-5 frame probe failed"; exit 1; }
 MVSV_TRI_TRACE=$O/tri_trace_c5.bin timeout -k 10 120 python tools/c5_frame.py > /dev/null 2>&1 && python tools/tri_trace.py $O/tri_trace_c5.bin > $O/tri_trace_c5.txt || { echo "c5 strip trace failed"; exit 1; }
-MVSV_TRI_TRACE=$O/tri_trace_b8.bin timeout -k 10 120 python bench.py --no-cpu-baseline --steps 1 --warmup 0 --inflight 1 --profile-steps 0 > /dev/null 2>&1 && python tools/tri_trace.py $O/tri_trace_b8.bin > $O/tri_trace_b8.txt || { echo "batch strip trace failed"; exit 1; }
+MVSV_TRI_TRACE=$O/tri_trace_b8.bin timeout -k 10 120 python bench.py --no-cpu-baseline --steps 1 --warmup 0 --inflight 1 --profile-steps 0 --no-configs > /dev/null 2>&1 && python tools/tri_trace.py $O/tri_trace_b8.bin > $O/tri_trace_b8.txt || { echo "batch strip trace failed"; exit 1; }
 timeout -k 10 60 ./tools/ubench/xcc_map 576 20 > $O/xcc_map.txt 2>&1 || { echo "xcc probe failed"; exit 1; }
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 10 --inflight 1 > $O/trace.log 2>&1 || { echo "trace failed"; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 10 --inflight 1 --no-configs > $O/trace.log 2>&1 || { echo "trace failed"; exit 1; }
 echo "round ok"
