@@ -36,7 +36,7 @@
  *                                     src/Stereosystem.cpp:193-237
  *   mvsv_reproject_device             Utility::calcCoordinate src/utility.cpp:176-198,
  *                                     per pixel (the loop of Utility::dmap2pcl :242-262)
- *   mvsv_calc_coordinate / _distance  Utility::calcCoordinate / calcDistance
+ *   mvsv_calc_coordinate(s) / _distance  Utility::calcCoordinate / calcDistance
  *   / _dmap_values                    src/utility.cpp:176-240 (host, one point)
  *   mvsv_write_ply                    ply::write src/ply.cpp:37-133 (MODE PLAIN,
  *                                     WITH_COLOR, WITH_COLOR_SHADING)
@@ -380,6 +380,11 @@ MVSV_API int mvsv_reproject_device(mvsv_ctx* ctx, int n, const int16_t* dmap, si
 /* Utility::calcCoordinate (one point, host): out = (X, Y, Z, 1). */
 MVSV_API void mvsv_calc_coordinate(float image_x, float image_y, float d_value, const float* Q,
                                    float* out4);
+/* calcCoordinate of n points at once (MeanDisparityDetection::detectObstacles'
+ * per-tile loop, src/MeanDisparityDetection.cpp:228-240): xyd = n x (image x,
+ * image y, disparity * 16), out = n x (X, Y, Z, 1); the same arithmetic as
+ * mvsv_calc_coordinate, one call instead of one per found tile. */
+MVSV_API void mvsv_calc_coordinates(int n, const float* xyd, const float* Q, float* out4);
 /* Utility::calcDistance: Z / 1000 of calcCoordinate, 0 when infinite. */
 MVSV_API float mvsv_calc_distance(float image_x, float image_y, float d_value, const float* Q);
 /* Utility::calcDMapValues: metric point (x, y, z) -> image x, y and disparity * 16. */

@@ -149,6 +149,7 @@ def _declare(lib, strict=True):
         "mvsv_resize": ([P, P, Z, I, I, ctypes.c_double, ctypes.c_double, P, Z], I),
         "mvsv_reproject_device": ([P, I, P, Z, Z, I, I, P, P, Z, Z], I),
         "mvsv_calc_coordinate": ([ctypes.c_float] * 3 + [P, P], None),
+        "mvsv_calc_coordinates": ([ctypes.c_int, P, P, P], None),
         "mvsv_calc_distance": ([ctypes.c_float] * 3 + [P], ctypes.c_float),
         "mvsv_calc_dmap_values": ([P, P, P, P, P], None),
         "mvsv_write_ply": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, P, Z, Z, I, P, Z,

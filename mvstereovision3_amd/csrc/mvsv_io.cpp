@@ -241,6 +241,11 @@ void mvsv_calc_coordinate(float image_x, float image_y, float d_value, const flo
     if (std::isinf(out[2] / 1000)) out[2] = 0.0f;
 }
 
+void mvsv_calc_coordinates(int n, const float* xyd, const float* Q, float* out4)
+{
+    for (int i = 0; i < n; i++) mvsv_calc_coordinate(xyd[3 * i], xyd[3 * i + 1], xyd[3 * i + 2], Q, out4 + 4 * i);
+}
+
 // [Utility::calcDistance] src/utility.cpp:200-222
 float mvsv_calc_distance(float image_x, float image_y, float d_value, const float* Q)
 {

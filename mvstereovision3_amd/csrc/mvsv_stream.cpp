@@ -18,8 +18,18 @@
 // its own HIP stream and scratch buffers), so up to n frame-batch launches run
 // concurrently and one fills the chip's gaps left by another's
 // latency-bound kernels.
+// The host copies of a frame (caller rows -> pinned slot on push, pinned map ->
+// caller rows on pop) are split over a small pool of copy threads that the
+// stream owns (MVSV_STREAM_COPY_THREADS, default 4 including the caller), so a
+// host whose single-core memcpy is slow still feeds the GPU at its rate.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "mvsv_internal.hpp"
@@ -28,6 +38,89 @@
 using namespace mvsv;
 
 static constexpr int kStreamMaxInflight = 4;
+static constexpr size_t kPoolMinBytes = (size_t)1 << 20;  // smaller copies stay on the caller's thread
+
+// Persistent row-copy pool: run(fn) calls fn(p, parts) once for every part
+// p < parts = size(), the calling thread taking parts too, and returns when
+// every worker has checked out of the run (so none touches fn or the part
+// counter after run returns).
+class CopyPool {
+  public:
+    explicit CopyPool(int threads)
+    {
+        for (int i = 1; i < threads; i++) workers_.emplace_back([this] { loop(); });
+    }
+    ~CopyPool()
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+    int size() const { return (int)workers_.size() + 1; }
+    void run(const std::function<void(int, int)>& fn)
+    {
+        const int parts = size();
+        if (parts == 1) {
+            fn(0, 1);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            fn_ = &fn;
+            next_.store(0, std::memory_order_relaxed);
+            active_ = parts - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        for (int p; (p = next_.fetch_add(1, std::memory_order_relaxed)) < parts;) fn(p, parts);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [&] { return active_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void loop()
+    {
+        long seen = 0;
+        for (;;) {
+            const std::function<void(int, int)>* fn;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                fn = fn_;
+            }
+            const int parts = size();
+            for (int p; (p = next_.fetch_add(1, std::memory_order_relaxed)) < parts;) (*fn)(p, parts);
+            std::lock_guard<std::mutex> g(m_);
+            if (--active_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int, int)>* fn_ = nullptr;
+    std::atomic<int> next_{0};
+    int active_ = 0;
+    long gen_ = 0;
+    bool stop_ = false;
+};
+
+// rows [0, H) of W-byte rows: src (stride ss) -> dst (stride ds), split by part
+static void copy_rows(uint8_t* dst, size_t ds, const uint8_t* src, size_t ss, size_t W, int H, int part,
+                      int parts)
+{
+    const int y0 = (int)((long)H * part / parts), y1 = (int)((long)H * (part + 1) / parts);
+    if (ds == W && ss == W) {
+        std::memcpy(dst + (size_t)y0 * W, src + (size_t)y0 * W, (size_t)(y1 - y0) * W);
+        return;
+    }
+    for (int y = y0; y < y1; y++) std::memcpy(dst + (size_t)y * ds, src + (size_t)y * ss, W);
+}
 
 struct mvsv_stream {
     mvsv_ctx* ctx = nullptr;
@@ -62,6 +155,7 @@ struct mvsv_stream {
     long head = 0, tail = 0;      // pushed / popped frame counters
     long launched = 0;            // frames whose compute is enqueued
     int batch = 1;
+    CopyPool* pool = nullptr;     // host copies of push / pop (nullptr: caller's thread only)
 };
 
 static void stream_free(mvsv_stream* st)
@@ -82,6 +176,7 @@ static void stream_free(mvsv_stream* st)
     if (st->rep) (void)hipHostFree(st->rep);
     if (st->up) (void)hipStreamDestroy(st->up);
     if (st->down) (void)hipStreamDestroy(st->down);
+    delete st->pool;
     delete st;
 }
 
@@ -133,6 +228,11 @@ int mvsv_stream_create(mvsv_ctx* ctx, int W, int H, const mvsv_sgbm_params* p, i
              hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
     }
     ok = ok && alloc_report(ctx, depth, &st->rep, &st->rep_dev) == MVSV_OK;
+    if (ok && px * 2 >= kPoolMinBytes) {
+        int threads = 4;
+        if (const char* v = std::getenv("MVSV_STREAM_COPY_THREADS")) threads = std::max(1, std::min(16, std::atoi(v)));
+        if (threads > 1) st->pool = new (std::nothrow) CopyPool(threads);
+    }
     if (!ok) {
         (void)hipGetLastError();
         stream_free(st);
@@ -279,10 +379,14 @@ int mvsv_stream_push(mvsv_stream* st, const uint8_t* L, size_t ls, const uint8_t
     auto& s = st->slots[st->head % st->slots.size()];
     const int W = st->W, H = st->H;
     // the slot's previous frame was popped, so its copies are complete
-    for (int y = 0; y < H; y++) {
-        std::memcpy(s.hL + (size_t)y * W, L + (size_t)y * ls, W);
-        std::memcpy(s.hR + (size_t)y * W, R + (size_t)y * rs, W);
-    }
+    auto copy_in = [&](int part, int parts) {
+        copy_rows(s.hL, W, L, ls, W, H, part, parts);
+        copy_rows(s.hR, W, R, rs, W, H, part, parts);
+    };
+    if (st->pool)
+        st->pool->run(copy_in);
+    else
+        copy_in(0, 1);
     const size_t px = (size_t)W * H;
     int rc;
     if ((rc = check_hip(ctx, hipMemcpyAsync(s.dL, s.hL, px, hipMemcpyHostToDevice, st->up), "stream H2D")) ||
@@ -321,9 +425,16 @@ int mvsv_stream_pop(mvsv_stream* st, int16_t* out, size_t os, float* means)
         return set_error(ctx, MVSV_E_TIMEOUT,
                          "stream frame: a strip-boundary wait of its SGBM launch gave up");
     }
-    if (out)
-        for (int y = 0; y < st->H; y++)
-            std::memcpy(out + (size_t)y * os, s.hOut + (size_t)y * st->W, (size_t)st->W * 2);
+    if (out) {
+        auto copy_out = [&](int part, int parts) {
+            copy_rows((uint8_t*)out, os * 2, (const uint8_t*)s.hOut, (size_t)st->W * 2, (size_t)st->W * 2, st->H,
+                      part, parts);
+        };
+        if (st->pool)
+            st->pool->run(copy_out);
+        else
+            copy_out(0, 1);
+    }
     if (means) {
         if (st->grid)
             std::memcpy(means, s.hMeans, 81 * sizeof(float));

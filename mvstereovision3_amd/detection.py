@@ -96,6 +96,9 @@ class MeanDisparityDetection:
                 br = (c * dx + dx, r * dy + dy)
                 self.mSubimageVec.append(Subimage(tl, br))
                 self.mFoundObstacles.append(Subimage(tl, br))
+        # detectObstacles' batched coordinate call: tile centres and Q as float32
+        self._centers = np.array([s.roi_center for s in self.mSubimageVec], np.float32).reshape(81, 2)
+        self._q16 = np.ascontiguousarray(self.mQ_32F.reshape(16))
         lo = Utility.calcDMapValues([0, 0, np.float32(min_distance) * np.float32(1000)], self.mQ_32F)
         hi = Utility.calcDMapValues([0, 0, np.float32(max_distance) * np.float32(1000)], self.mQ_32F)
         self.mRangeDisparity = (lo.dValue, hi.dValue)
@@ -140,10 +143,9 @@ class MeanDisparityDetection:
             mode = MEAN_VALUE
         if mode == MEAN_VALUE:
             self.mDetectionMode = MEAN_VALUE
-            self.mMeanMap = []
-            for i, s in enumerate(self.mSubimageVec):
-                s.value = float(m[i])
-                self.mMeanMap.append(float(m[i]))
+            self.mMeanMap = m.tolist()
+            for s, v in zip(self.mSubimageVec, self.mMeanMap):
+                s.value = v
 
     def _grid(self, dMap):
         if type(dMap).__module__.startswith("torch"):
@@ -171,15 +173,21 @@ class MeanDisparityDetection:
             return printed
         if self.mDetectionMode != MEAN_VALUE:
             return printed
-        self.mFoundObstacles = []
-        self.mFoundPoints = []
         lo, hi = np.float32(self.mRangeDisparity[0]), np.float32(self.mRangeDisparity[1])
-        for i, mean in enumerate(self.mMeanMap):
-            if np.float32(mean) < lo and np.float32(mean) > hi:
-                s = self.mSubimageVec[i]
-                self.mFoundObstacles.append(s)
-                v = dMapValues(mean, s.roi_center[0], s.roi_center[1])
-                self.mFoundPoints.append(Utility.calcCoordinate(v, self.mQ_32F))
+        # the reference's per-tile test (float32 compares) over all 81 means at
+        # once, then every found tile's coordinate in one native call
+        means = np.asarray(self.mMeanMap, np.float32)
+        found = np.flatnonzero((means < lo) & (means > hi))
+        self.mFoundObstacles = [self.mSubimageVec[i] for i in found]
+        self.mFoundPoints = []
+        if found.size:
+            xyd = np.empty((found.size, 3), np.float32)
+            xyd[:, 0] = self._centers[found, 0]
+            xyd[:, 1] = self._centers[found, 1]
+            xyd[:, 2] = means[found]
+            pts = np.empty((found.size, 4), np.float32)
+            lib().mvsv_calc_coordinates(int(found.size), xyd.ctypes.data, self._q16.ctypes.data, pts.ctypes.data)
+            self.mFoundPoints = list(pts)
         if self.mFoundPoints and write_pcl:
             c = self.mObstacleCounter
             prefix = "000" if c < 10 else ("00" if c < 100 else "0")

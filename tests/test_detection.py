@@ -70,3 +70,27 @@ def test_mean_distance_falls_through_to_mean_value(mvsv):
     s = m.getSubimageVec()[5]
     assert m.getMeanDistanceMap()[5] == Utility.calcDistance(
         dMapValues(means[5], s.roi_center[0], s.roi_center[1]), Q_REF, 0)
+
+
+def test_detect_obstacles_batched_points_match_per_tile(mvsv):
+    """detectObstacles' one native call for all found tiles (mvsv_calc_coordinates)
+    gives the points of the reference's per-tile Utility::calcCoordinate loop
+    (src/MeanDisparityDetection.cpp:228-240), bit for bit, on many found tiles."""
+    from mvstereovision3_amd.utility import Utility, dMapValues
+    m = mvsv.MeanDisparityDetection()
+    m.init((960, 1152), Q_REF, 0.1, 1.5)
+    lo, hi = (np.float32(v) for v in m.mRangeDisparity)
+    rng = np.random.default_rng(77)
+    means = rng.uniform(float(hi) - 50, float(lo) + 50, 81).astype(np.float32)
+    means[:4] = [hi, lo, np.nextafter(hi, np.float32(1e9)), np.nextafter(lo, np.float32(-1e9))]
+    m.build(np.zeros((960, 1152), np.int16), 0, m.MEAN_VALUE, means=means)
+    m.detectObstacles(write_pcl=False)
+    want_tiles, want_pts = [], []
+    for i, s in enumerate(m.getSubimageVec()):
+        if means[i] < lo and means[i] > hi:
+            want_tiles.append(s.tl)
+            want_pts.append(Utility.calcCoordinate(dMapValues(means[i], *s.roi_center), m.mQ_32F))
+    assert [s.tl for s in m.getFoundObstacles()] == want_tiles and len(want_tiles) > 20
+    assert len(m.mFoundPoints) == len(want_pts)
+    for got, want in zip(m.mFoundPoints, want_pts):
+        assert got.dtype == np.float32 and np.array_equal(got.view(np.uint32), want.view(np.uint32))
