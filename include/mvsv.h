@@ -270,6 +270,10 @@ MVSV_API int mvsv_stream_push(mvsv_stream* s, const uint8_t* left, size_t left_s
 /* waits for the oldest pending frame; out (int16, stride in elements) and means
  * (81 floats) may be NULL */
 MVSV_API int mvsv_stream_pop(mvsv_stream* s, int16_t* out, size_t out_stride, float* means);
+/* pop without the map copy: *map points at the frame's int16 map in the stream's
+ * pinned host slot (width elements per row, rows contiguous), valid until the
+ * next push (which may reuse the slot); means (81 floats) may be NULL */
+MVSV_API int mvsv_stream_pop_view(mvsv_stream* s, const int16_t** map, float* means);
 MVSV_API int mvsv_stream_pending(const mvsv_stream* s);
 MVSV_API void mvsv_stream_destroy(mvsv_stream* s);
 

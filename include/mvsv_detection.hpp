@@ -288,6 +288,14 @@ public:
         check(mvsv_stream_pop(s_, reinterpret_cast<int16_t*>(disparity.data), disparity.step / 2, means81),
               ctx_);
     }
+    // the oldest frame's map in the stream's pinned host slot (width x height
+    // int16, no copy), valid until the next push
+    const int16_t* popView(float* means81 = nullptr)
+    {
+        const int16_t* map = nullptr;
+        check(mvsv_stream_pop_view(s_, &map, means81), ctx_);
+        return map;
+    }
 
 private:
     mvsv_ctx* ctx_;

@@ -138,6 +138,7 @@ def _declare(lib, strict=True):
         "mvsv_stream_set_inflight": ([P, I], I),
         "mvsv_stream_push": ([P, P, Z, P, Z], I),
         "mvsv_stream_pop": ([P, P, Z, P], I),
+        "mvsv_stream_pop_view": ([P, P, P], I),
         "mvsv_stream_pending": ([P], I),
         "mvsv_stream_destroy": ([P], None),
         "mvsv_remap_device": ([P, I, P, Z, Z, I, I, P, P, Z, P, Z, Z, I, I], I),

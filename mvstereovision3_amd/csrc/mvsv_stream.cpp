@@ -400,14 +400,14 @@ int mvsv_stream_push(mvsv_stream* st, const uint8_t* L, size_t ls, const uint8_t
     return MVSV_OK;
 }
 
-int mvsv_stream_pop(mvsv_stream* st, int16_t* out, size_t os, float* means)
+// Wait for the oldest pending frame and release its slot: its status, and the
+// slot whose pinned map / means hold the result (valid until the slot's reuse).
+static int stream_pop_slot(mvsv_stream* st, mvsv_stream::Slot** slot)
 {
-    if (!st) return MVSV_E_INVALID_ARG;
     mvsv_ctx* ctx = st->ctx;
     if (st->head == st->tail) return set_error(ctx, MVSV_E_INVALID_ARG, "stream empty");
-    if (out && os < (size_t)st->W) return set_error(ctx, MVSV_E_INVALID_ARG, "stride smaller than width");
     auto& s = st->slots[st->tail % st->slots.size()];
-    DeviceGuard dev_guard(ctx->device);
+    *slot = &s;
     int rc = MVSV_OK;
     if (st->tail >= st->launched && (rc = stream_launch(st))) return rc;  // partial group
     rc = check_hip(ctx, hipEventSynchronize(s.done), "stream sync");
@@ -425,6 +425,27 @@ int mvsv_stream_pop(mvsv_stream* st, int16_t* out, size_t os, float* means)
         return set_error(ctx, MVSV_E_TIMEOUT,
                          "stream frame: a strip-boundary wait of its SGBM launch gave up");
     }
+    return MVSV_OK;
+}
+
+static void stream_means(const mvsv_stream* st, const mvsv_stream::Slot& s, float* means)
+{
+    if (!means) return;
+    if (st->grid)
+        std::memcpy(means, s.hMeans, 81 * sizeof(float));
+    else
+        std::memset(means, 0, 81 * sizeof(float));
+}
+
+int mvsv_stream_pop(mvsv_stream* st, int16_t* out, size_t os, float* means)
+{
+    if (!st) return MVSV_E_INVALID_ARG;
+    if (out && os < (size_t)st->W) return set_error(st->ctx, MVSV_E_INVALID_ARG, "stride smaller than width");
+    DeviceGuard dev_guard(st->ctx->device);
+    mvsv_stream::Slot* sp = nullptr;
+    int rc = stream_pop_slot(st, &sp);
+    if (rc) return rc;
+    const auto& s = *sp;
     if (out) {
         auto copy_out = [&](int part, int parts) {
             copy_rows((uint8_t*)out, os * 2, (const uint8_t*)s.hOut, (size_t)st->W * 2, (size_t)st->W * 2, st->H,
@@ -435,12 +456,20 @@ int mvsv_stream_pop(mvsv_stream* st, int16_t* out, size_t os, float* means)
         else
             copy_out(0, 1);
     }
-    if (means) {
-        if (st->grid)
-            std::memcpy(means, s.hMeans, 81 * sizeof(float));
-        else
-            std::memset(means, 0, 81 * sizeof(float));
-    }
+    stream_means(st, s, means);
+    return MVSV_OK;
+}
+
+int mvsv_stream_pop_view(mvsv_stream* st, const int16_t** map, float* means)
+{
+    if (!st || !map) return MVSV_E_INVALID_ARG;
+    *map = nullptr;
+    DeviceGuard dev_guard(st->ctx->device);
+    mvsv_stream::Slot* sp = nullptr;
+    int rc = stream_pop_slot(st, &sp);
+    if (rc) return rc;
+    *map = sp->hOut;
+    stream_means(st, *sp, means);
     return MVSV_OK;
 }
 

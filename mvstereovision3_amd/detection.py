@@ -256,7 +256,19 @@ class DisparityStream:
                                      R.strides[0]), self._ctx.handle)
 
     def pop(self, copy_map=True):
-        """(map, means) of the oldest frame; copy_map=False returns (None, means)."""
+        """(map, means) of the oldest frame; copy_map=False returns (None, means);
+        copy_map="view" returns a read-only view of the map in the stream's pinned
+        host slot (no host copy), valid until the next push."""
+        if copy_map == "view":
+            ptr = ctypes.c_void_p()
+            means = np.empty(81, np.float32) if self._grid else None
+            check(lib().mvsv_stream_pop_view(self._h, ctypes.byref(ptr),
+                                             means.ctypes.data if means is not None else None),
+                  self._ctx.handle)
+            buf = (ctypes.c_int16 * (self.width * self.height)).from_address(ptr.value)
+            view = np.ctypeslib.as_array(buf).reshape(self.height, self.width)
+            view.flags.writeable = False
+            return view, means
         out = np.empty((self.height, self.width), np.int16) if copy_map else None
         means = np.empty(81, np.float32) if self._grid else None
         check(lib().mvsv_stream_pop(self._h, out.ctypes.data if out is not None else None, self.width,

@@ -537,3 +537,51 @@ def test_stereosystem_rectified_pair_then_sgbm(gpu, mvsv, oracle):
     p = dict(m.params())
     p.pop("variant")
     assert np.array_equal(d, oracle.sgbm(np.ascontiguousarray(sip.mLeft), np.ascontiguousarray(sip.mRight), p))
+
+
+@pytest.mark.parametrize("threads", ["1", "3"])
+def test_stream_copy_pool_and_pop_view(gpu, mvsv, oracle, threads, monkeypatch):
+    """Frames large enough for the stream's host copy pool (>= 1 MiB maps), strided
+    input rows, pops alternating between a copy (mvsv_stream_pop) and a view of the
+    pinned slot (mvsv_stream_pop_view): every map equals the synchronous call's, the
+    first also the oracle's, and a view popped after the last push stays intact."""
+    monkeypatch.setenv("MVSV_STREAM_COPY_THREADS", threads)
+    W, H, D = 1024, 528, 64
+    m = mvsv.StereoSGBM.create(0, D, 5, 8 * 25, 32 * 25)
+    roi_u, _ = mvsv.create_dmap_rois((H, W), D)
+    depth = 3
+    st = mvsv.DisparityStream(m, W, H, depth=depth, grid_roi=roi_u)
+    frames = []
+    for i in range(6):
+        L, R = mvsv.synth_pair(SEED0 + 90 + i, W, H, 0, D)
+        pad = np.zeros((H, W + 40), np.uint8)
+        padR = np.zeros((H, W + 24), np.uint8)
+        pad[:, 7:7 + W] = L
+        padR[:, 3:3 + W] = R
+        frames.append((pad[:, 7:7 + W], padR[:, 3:3 + W]))  # row strides > width
+    got = []
+    for i, (L, R) in enumerate(frames):
+        if st.pending() == depth:
+            k = len(got)
+            d, means = st.pop(copy_map="view" if k % 2 else True)
+            got.append((d.copy(), np.array(d, copy=False), means))
+        st.push(L, R)
+    while st.pending():
+        k = len(got)
+        d, means = st.pop(copy_map="view" if k % 2 else True)
+        got.append((d.copy(), np.array(d, copy=False), means))
+    assert len(got) == len(frames)
+    for i, ((L, R), (d, live, means)) in enumerate(zip(frames, got)):
+        want = m.compute(np.ascontiguousarray(L), np.ascontiguousarray(R))
+        assert np.array_equal(d, want), f"frame {i}: " + report(d, want)
+        if i == 0:
+            p = dict(m.params())
+            p.pop("variant")
+            assert np.array_equal(d, oracle.sgbm(np.ascontiguousarray(L), np.ascontiguousarray(R), p))
+        x0, y0, x1, y1 = roi_u
+        assert np.array_equal(means, oracle.mean_disparity_grid(np.ascontiguousarray(want[y0:y1, x0:x1])))
+    # views popped after the last push: still the frame's map
+    for i in range(len(frames) - depth, len(frames)):
+        if i % 2:
+            assert np.array_equal(got[i][1], got[i][0])
+    st.close()

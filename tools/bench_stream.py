@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--batch", type=int, default=8, help="frames per SGBM launch (mvsv_stream_set_batch)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="launches computed concurrently (mvsv_stream_set_inflight)")
+    ap.add_argument("--pop", choices=["view", "copy"], default="view",
+                    help="map delivery: a read-only view of the pinned slot (mvsv_stream_pop_view) "
+                         "or a copy into a fresh array (mvsv_stream_pop)")
     ap.add_argument("--host-probe", choices=["full", "no-post", "no-copy"], default="full",
                     help="diagnostics: skip the detection post-pass, or also the map copy of pop")
     ap.add_argument("--width", type=int, default=1280)
@@ -60,7 +63,7 @@ def main():
         if a.host_probe == "no-copy":
             st.pop(copy_map=False)
         else:
-            d, means = st.pop()
+            d, means = st.pop(copy_map="view" if a.pop == "view" else True)
         t2 = time.perf_counter()
         if a.host_probe == "full":
             det.build(d, 0, det.MEAN_VALUE, means=means)
@@ -104,7 +107,7 @@ def main():
     print(json.dumps({
         "workload": f"config5_stream_{W}x{H}_d{D}_mode_sgbm",
         "frames": a.frames, "depth": a.depth, "batch": a.batch, "inflight": a.inflight,
-        "host_probe": a.host_probe,
+        "host_probe": a.host_probe, "pop": a.pop,
         "stream_fps": round(a.frames / wall, 2),
         "stream_mpix_s": round(a.frames * W * H / wall / 1e6, 2),
         "stream_ms_per_frame": round(wall / a.frames * 1e3, 3),
