@@ -244,15 +244,6 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(int16_t* __restrict_
     int* tl = tilew + f * npix;
     int* sz = size + f * npix;
     uint16_t* lr = lroot + f * npix;
-    // the block's tile roots go to the compact root list (list[0] = count)
-    // with ONE global atomic per block: per (wave, k) ballots, an exclusive
-    // scan of their counts in LDS, one atomicAdd by thread 0 (16x fewer atomics
-    // on the single counter than one per wave and row pair; measured neutral on
-    // the bench workload, profiles/r04/post04)
-    __shared__ unsigned sp_cnt[4 * 4 + 1];  // [k][wave] root counts, then the block's base
-    const int wv = threadIdx.x >> 6;
-    bool isroot[4];
-    unsigned long long rm[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int ly = ty + 8 * k, li = ly * kSpTile + tx;
@@ -261,34 +252,22 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(int16_t* __restrict_
         const int gi = gy * W + gx;
         if (in) lr[gi] = (uint16_t)(root[k] >= 0 ? root[k] : 0xffff);
         const int c = lcnt[li];
-        isroot[k] = in && c > 0;
-        if (isroot[k]) {
+        const bool isroot = in && c > 0;
+        if (isroot) {
             par[gi] = gi;
             tl[gi] = c;
             sz[gi] = 0;
         }
-        rm[k] = __ballot(isroot[k]);
-        if (lane == 0) sp_cnt[k * 4 + wv] = (unsigned)__popcll(rm[k]);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned tot = 0;
-        for (int i = 0; i < 16; i++) {
-            const unsigned c = sp_cnt[i];
-            sp_cnt[i] = tot;
-            tot += c;
+        // wave-aggregated append to the compact root list (list[0] = count)
+        const unsigned long long m = __ballot(isroot);
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            unsigned base = 0;
+            if (lane == leader) base = atomicAdd(list, (unsigned)__popcll(m));
+            base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
+            if (isroot)
+                list[1 + base + (unsigned)__popcll(m & ((1ull << lane) - 1ull))] = (unsigned)(f * npix + gi);
         }
-        sp_cnt[16] = tot ? atomicAdd(list, tot) : 0u;
-    }
-    __syncthreads();
-    const unsigned base = sp_cnt[16];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        if (!isroot[k]) continue;
-        const int ly = ty + 8 * k;
-        const int gi = (y0 + ly) * W + x0 + tx;
-        list[1 + base + sp_cnt[k * 4 + wv] + (unsigned)__popcll(rm[k] & ((1ull << lane) - 1ull))] =
-            (unsigned)(f * npix + gi);
     }
 }
 
