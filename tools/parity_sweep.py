@@ -79,6 +79,8 @@ def main():
         _lib.set_option(_lib.OPT_PATH_SCHEDULE, sched)
         _lib.set_option(_lib.OPT_STRIP_WAVES, waves)
         _lib.set_option(_lib.OPT_STRIP_TICKETS, int(rng.integers(0, 2)))
+        res = int(rng.choice([1, 1, 1, 0]))  # cost residual plane where exact (round 4) / forced off
+        _lib.set_option(_lib.OPT_COST_RESIDUAL, res)
         try:
             if n == 1:
                 got = m.compute(*pairs[0])[None]
@@ -94,7 +96,7 @@ def main():
             continue
         p = {k: v for k, v in m.params().items() if k != "variant"}
         for j, (L, R) in enumerate(pairs):
-            tag = f"sgbm #{i} frame {j}/{n} {H}x{W} {kw} variant={variant} sched={sched} waves={waves}"
+            tag = f"sgbm #{i} frame {j}/{n} {H}x{W} {kw} variant={variant} sched={sched} waves={waves} res={res}"
             jobs.append((tag, got[j], pool.submit(pyoracle.sgbm, L, R, p, variant)))
     _lib.set_option(_lib.OPT_PATH_SCHEDULE, 0)
     _lib.set_option(_lib.OPT_STRIP_WAVES, 0)
@@ -104,14 +106,17 @@ def main():
         n = int(rng.choice([4, 8])) if W == 640 else int(rng.choice([2, 4]))
         D = int(rng.choice([64, 128, 256]))
         kw = dict(minDisparity=int(rng.integers(-4, 4)), numDisparities=D,
-                  blockSize=int(rng.choice([3, 5, 9, 13])), P1=int(rng.choice([0, 8, 648])),
-                  P2=int(rng.choice([0, 32, 2592])), disp12MaxDiff=int(rng.integers(-1, 3)),
+                  blockSize=int(rng.choice([3, 5, 9, 13])), P1=int(rng.choice([0, 2, 8, 648])),
+                  P2=int(rng.choice([0, 5, 32, 2592])), disp12MaxDiff=int(rng.integers(-1, 3)),
                   preFilterCap=int(rng.choice([0, 31, 63])), uniquenessRatio=int(rng.choice([0, 10])),
                   speckleWindowSize=int(rng.choice([0, 150])), speckleRange=2, mode=int(rng.integers(0, 2)))
         m = mvsv.StereoSGBM.create(**kw)
         tickets = int(rng.integers(0, 2))  # strip order of launches larger than the CU count
         _lib.set_option(_lib.OPT_STRIP_TICKETS, tickets)
         kw["strip_tickets"] = tickets
+        res = int(rng.choice([1, 1, 1, 0]))
+        _lib.set_option(_lib.OPT_COST_RESIDUAL, res)
+        kw["cost_residual"] = res
         pairs = [mvsv.synth_pair(int(rng.integers(0, 1 << 30)), W, H, max(kw["minDisparity"], 0), D)
                  for _ in range(n)]
         Lb = torch.from_numpy(np.stack([q[0] for q in pairs])).to(dev)
@@ -123,6 +128,7 @@ def main():
         for j, (L, R) in enumerate(pairs):
             jobs.append((f"large #{i} frame {j}/{n} {W}x{H} {kw}", got[j], pool.submit(pyoracle.sgbm, L, R, p)))
     _lib.set_option(_lib.OPT_STRIP_TICKETS, 1)
+    _lib.set_option(_lib.OPT_COST_RESIDUAL, 1)
 
     for i in range(a.bm):
         H, W = int(rng.integers(24, 200)), int(rng.integers(80, 400))
@@ -157,7 +163,9 @@ def main():
     _lib.set_option(_lib.OPT_BM_TILE_ROWS, 0)
     mvsv.synchronize()
 
-    for tag, got, fut in jobs:
+    for done, (tag, got, fut) in enumerate(jobs):
+        if done % 50 == 0:
+            print(f"checked {done} / {len(jobs)}", flush=True)  # progress (a quiet run looks hung)
         try:
             want = fut.result()
         except ValueError as ex:
