@@ -27,6 +27,12 @@ __device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b)
 {
     return as_u(__builtin_elementwise_min(as_s2(a), as_s2(b)));
 }
+// Two u16 halves added / subtracted as one 32-bit word: exact only where no
+// half carries or borrows (each call site states why).  v_add_u32 / v_sub_u32
+// issue at twice the rate of the VOP3P packed ops (2.5 vs 4.2 cycles per
+// wave-instruction, tools/ubench/valu_rate.hip).
+__device__ __forceinline__ uint32_t add2_nc(uint32_t a, uint32_t b) { return a + b; }
+__device__ __forceinline__ uint32_t sub2_nb(uint32_t a, uint32_t b) { return a - b; }
 __device__ __forceinline__ int lo16(uint32_t v) { return (int)(int16_t)(v & 0xffffu); }
 __device__ __forceinline__ int hi16(uint32_t v) { return (int)(int16_t)(v >> 16); }
 __device__ __forceinline__ uint32_t pk2(int lo, int hi)

@@ -205,11 +205,14 @@ __device__ __forceinline__ uint32_t seg_min_u16x2(uint32_t v, int lanes)
 // ---------------------------------------------------------------------------
 
 // BT cost of one channel for a disparity pair: u* broadcast, v* per half.
+// The distance of u to the interval [v0, v1] is max(u - v1, v0 - u, 0); with
+// v0 <= v1 at most one of the two saturated differences is non-zero, so their
+// sum (bytes: no half carries -- a full-rate 32-bit add) is that maximum.
 __device__ __forceinline__ uint32_t bt_pair(uint32_t u, uint32_t u0, uint32_t u1, uint32_t v,
                                            uint32_t v0, uint32_t v1)
 {
-    uint32_t c0 = pk_max_u16(pk_subsat_u16(u, v1), pk_subsat_u16(v0, u));
-    uint32_t c1 = pk_max_u16(pk_subsat_u16(v, u1), pk_subsat_u16(u0, v));
+    uint32_t c0 = add2_nc(pk_subsat_u16(u, v1), pk_subsat_u16(v0, u));
+    uint32_t c1 = add2_nc(pk_subsat_u16(v, u1), pk_subsat_u16(u0, v));
     return pk_min_u16(c0, c1);
 }
 
@@ -384,7 +387,8 @@ __device__ __forceinline__ uint32_t bt_cost2(uint4 u4, uint2 u2, uint4 v4, uint2
     const uint32_t cb = bt_pair(u4.w, u2.x, u2.y, v4.w, v2.x, v2.y);
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     const u16x2 two = {2, 2};
-    return pk_add_u16(ca, __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, cb) >> two));
+    // ca <= 2 ftzero <= 126, cb >> 2 <= 63: the halves never carry (full-rate add)
+    return add2_nc(ca, __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, cb) >> two));
 }
 
 template <int NR, int STG, int PPC>
@@ -592,7 +596,11 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                 }
                 uint32_t h = 0;
 #pragma unroll
-                for (int q = 0; q < NR; q++) h = pk_add_u16(h, wv[q]);
+                // packed sums as 32-bit words (full rate): a pixel cost is <= 189,
+                // so a horizontal sum h <= 15 * 189 and a window sum <= 15 * 15 * 189
+                // = 42525 < 2^16 -- no half ever carries or borrows (the slide
+                // subtracts a term the sum holds)
+                for (int q = 0; q < NR; q++) h = add2_nc(h, wv[q]);
                 const bool emit = k >= NR - 1;
                 uint32_t* orow = obase + (size_t)k * ostride;
                 // MODE_HH: OpenCV 3.4 leaves P2 in the rows it never recomputes
@@ -603,8 +611,8 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                 uint32_t ov[kCost2Run];
 #pragma unroll
                 for (int i = 0; i < kCost2Run; i++) {
-                    if (i > 0) h = pk_sub_u16(pk_add_u16(h, wv[i + NR - 1]), wv[i - 1]);
-                    csum[i] = pk_add_u16(pk_sub_u16(csum[i], ring[s][i]), h);
+                    if (i > 0) h = sub2_nb(add2_nc(h, wv[i + NR - 1]), wv[i - 1]);
+                    csum[i] = add2_nc(sub2_nb(csum[i], ring[s][i]), h);
                     ring[s][i] = h;
                     const bool pin = pin_row || (i == 0 && pin_x0);
                     ov[i] = pin ? p2x2 : pk_add_u16(p2x2, csum[i]);
@@ -657,11 +665,13 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                     // column pairs; one word holds columns 0 and 1's residual
                     // bytes R[2p] | R[2p+1] << 4 in bits 0-7 and 16-23
                     const uint32_t p2x3 = pk_add_u16(pk_add_u16(p2x2, p2x2), p2x2);
-                    const uint32_t Am = pk_sub_u16(A, p2x2), Bm = pk_sub_u16(B, p2x2);
-                    const uint32_t r01 = pk_min_u16(pk_sub_u16(Plo01, Am), p2x3) |
-                                         (pk_min_u16(pk_sub_u16(Phi01, Am), p2x3) << 4);
-                    const uint32_t r23 = pk_min_u16(pk_sub_u16(Plo23, Bm), p2x3) |
-                                         (pk_min_u16(pk_sub_u16(Phi23, Bm), p2x3) << 4);
+                    // (residual runs are no-wrap: P2 <= m <= C, so the 32-bit
+                    // subtractions never borrow)
+                    const uint32_t Am = sub2_nb(A, p2x2), Bm = sub2_nb(B, p2x2);
+                    const uint32_t r01 = pk_min_u16(sub2_nb(Plo01, Am), p2x3) |
+                                         (pk_min_u16(sub2_nb(Phi01, Am), p2x3) << 4);
+                    const uint32_t r23 = pk_min_u16(sub2_nb(Plo23, Bm), p2x3) |
+                                         (pk_min_u16(sub2_nb(Phi23, Bm), p2x3) << 4);
                     uint8_t* rrow = Rv + (orow - (uint32_t*)C);  // byte (pixel, pair) = dword (pixel, pair) of C
                     const uint32_t rw[kCost2Run] = {r01, r01 >> 16, r23, r23 >> 16};
 #pragma unroll
@@ -1228,20 +1238,26 @@ template <bool NW>
 __device__ __forceinline__ void sgm_pair(uint32_t lp, uint32_t nb, uint32_t delta2, uint32_t p1x2,
                                          uint32_t c, uint32_t& ln, uint32_t& tu)
 {
-    const uint32_t m = pk_min(lp, pk_add_sat(nb, p1x2));
     if constexpr (NW) {
+        // full-rate 32-bit forms, exact here: nb <= 0x7fff and P1 < 0x8000, so
+        // nb + P1 never carries out of its half (the unsigned min then equals
+        // min(L, sat(nb + P1)) because L <= 0x7fff); u <= P2 <= C (every cost
+        // of the no-wrap regime is P2 + a window sum, every residual is in
+        // [P2, 3 P2]), so C - u never borrows
+        const uint32_t m = pk_min_u16(lp, add2_nc(nb, p1x2));
         tu = pk_subsat_u16(delta2, m);
-        ln = pk_sub_sat(c, tu);
+        ln = sub2_nb(c, tu);
     } else {
+        const uint32_t m = pk_min(lp, pk_add_sat(nb, p1x2));
         tu = pk_sub_sat(pk_min(m, delta2), delta2);
         ln = pk_add_sat(tu, c);
     }
 }
-// delta = t + P2 (general) = P2 - u (NW), in [0, P2]
+// delta = t + P2 (general) = P2 - u (NW, u <= P2: no borrow), in [0, P2]
 template <bool NW>
 __device__ __forceinline__ uint32_t sgm_delta(uint32_t tu, uint32_t p2x2)
 {
-    return NW ? pk_sub_u16(p2x2, tu) : pk_add_u16(tu, p2x2);
+    return NW ? sub2_nb(p2x2, tu) : pk_add_u16(tu, p2x2);
 }
 // the packed delta = (short)(minLp + P2) of the next step
 template <bool NW>
@@ -1796,7 +1812,8 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU + (RES && WV
         };
         // sum of the three deltas t_r + P2 = 3 P2 - (u_a + u_b + u_c) (no-wrap)
         // or t_a + t_b + t_c + 3 P2, exact in u16 wrap arithmetic
-        auto acc = [&](uint32_t o, uint32_t u) -> uint32_t { return NW ? pk_sub_u16(o, u) : pk_add_u16(o, u); };
+        // (no-wrap: 3 P2 minus three u <= P2 each never borrows -> one full-rate v_sub_u32)
+        auto acc = [&](uint32_t o, uint32_t u) -> uint32_t { return NW ? sub2_nb(o, u) : pk_add_u16(o, u); };
         uint32_t o[NP];
 #if MVSV_TRI_STEP_SEQ
         {  // (1, sy): the strip's own column, state in registers
@@ -2275,8 +2292,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
         uint32_t key = 0x7fffffffu;
 #pragma unroll
         for (int p = 0; p < NP; p++) {
-            const uint32_t cbv = pk_sub_u16(c[p], p2x2);
-            const uint32_t sv = pk_mad_u16_clamp(cbv, ndm1, pk_add_u16(ln[p], acc[p]));
+            // residual form (RESF): R >= P2, L + deltas <= 4 P2 + 7 P2 -- the
+            // full-rate 32-bit sub / add never borrow or carry
+            const uint32_t cbv = RESF ? sub2_nb(c[p], p2x2) : pk_sub_u16(c[p], p2x2);
+            const uint32_t sv = pk_mad_u16_clamp(cbv, ndm1, RESF ? add2_nc(ln[p], acc[p]) : pk_add_u16(ln[p], acc[p]));
             st[p] = pk_min_u16(sv, 0x7fff7fffu);
             lp[p] = ln[p];
             const uint32_t klo = (st[p] << 16) | subk[2 * p];
