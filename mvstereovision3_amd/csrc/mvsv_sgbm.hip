@@ -2956,7 +2956,16 @@ int launch_paths16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t
     if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
     AccT* dummy = (AccT*)ctx->dummy.ptr;
     const size_t plane = (size_t)n * H * e.W1 * e.D;
-    if (use_strips(ctx, e, H)) return launch_paths_tri<NP, AccT, false>(ctx, n, H, W, e, Cv, Cv, Av, plane, raw);
+    // u8 / u16 planes (P2 > 5) at D = 256 (liveDisparity, config 5): the
+    // no-wrap recurrence wherever no int16 can wrap -- its adds / subtracts
+    // run at the full 32-bit rate, so it is the cheaper form here too (one
+    // frame 2.04 -> 1.99 ms, profiles/r04/c5ab04); other D keep the general
+    // form (compile time)
+    if (use_strips(ctx, e, H)) {
+        if constexpr (NP == 8)
+            if (sgbm_no_wrap(e)) return launch_paths_tri<NP, AccT, true>(ctx, n, H, W, e, Cv, Cv, Av, plane, raw);
+        return launch_paths_tri<NP, AccT, false>(ctx, n, H, W, e, Cv, Cv, Av, plane, raw);
+    }
     const int ndir = e.fullDP ? 7 : 4;
     for (int k = 0; k < ndir; k++) {
         int dx = e.fullDP ? dirs_hh[k][0] : dirs_sgbm[k][0];
