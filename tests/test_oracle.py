@@ -243,3 +243,32 @@ def test_cost_residual_invariance(seed):
     S2 = n * (Rr - P2) + Spp
     assert np.array_equal(S.argmin(axis=-1), S2.argmin(axis=-1))
     assert np.array_equal(S.min(axis=-1), S2.min(axis=-1) + n * (m[..., 0] - P2))
+
+
+@pytest.mark.parametrize("cap", [15, 63])
+def test_fullrate_bounds_of_the_cost_sums(cap):
+    """The bounds behind the cost kernel's full-rate 32-bit sums and the BT
+    distance rewrite, on the numpy twin with adversarial input
+    (alternating 0 / 255 columns and rows: the largest Sobel and raw-channel
+    intervals): every pixel cost <= 2*ftzero + 255 // 4 <= 189, so a 15x15 window sum
+    stays < 2^16; and max(u - v1, v0 - u, 0) == sat(u - v1) + sat(v0 - u) for
+    every interval (v0 <= v1)."""
+    from oracle import twin
+    rng = np.random.default_rng(cap)
+    H, W, D = 20, 90, 32
+    L = np.where((np.arange(W)[None, :] + np.arange(H)[:, None]) % 2, 255, 0).astype(np.uint8)
+    R = np.where(rng.random((H, W)) < 0.5, 255, 0).astype(np.uint8)
+    p = dict(min_disparity=0, num_disparities=D, block_size=3, p1=2, p2=5, disp12_max_diff=1,
+             pre_filter_cap=cap, uniqueness_ratio=0, speckle_window_size=0, speckle_range=0, mode=1)
+    e = twin.sgbm_effective(p, W)
+    pix = twin.sgbm_pixel_cost(L, R, e)
+    assert pix.max() <= 2 * e["ftzero"] + 255 // 4 <= 189
+    assert 15 * 15 * 189 < 1 << 16
+    # the interval-distance identity on every (u, [v0, v1]) of bytes
+    u = np.arange(256, dtype=np.int16)[:, None, None]
+    v0 = np.arange(256, dtype=np.int16)[None, :, None]
+    v1 = np.arange(256, dtype=np.int16)[None, None, :]
+    ok = v0 <= v1
+    lhs = np.maximum(np.maximum(u - v1, v0 - u), 0)
+    rhs = np.maximum(u - v1, 0) + np.maximum(v0 - u, 0)
+    assert np.array_equal(np.where(ok, lhs, 0), np.where(ok, rhs, 0))
