@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of library variants (variants/NAME.so; "new" = the in-tree build):
 # bench stage times, one batch in flight, two alternating rounds.
-# Usage (on the box): bash tools/gpu_ab_libs.sh TAG "new nolroot nocount"
+# Usage (on the box): bash tools/gpu_ab_libs.sh TAG "new prev"
 set -o pipefail
 TAG=${1:-ab}; VARS=${2:-new}
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp; cd $R

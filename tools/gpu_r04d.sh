@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 4, first session on the cost-residual build: new tests, full GPU suite,
-# same-box A/B (round-3 library vs this build with the residual on / off),
-# PMC traffic (FETCH_SIZE / WRITE_SIZE passes), bench, kernel-trace stats.
+# Round 4, strip-launch session: new tests, full GPU suite, same-box A/B of the
+# round-3 library vs this build with the L->R lines on the aux stream (aux2) and
+# narrow strips (nar, nar2), PMC traffic, bench, kernel-trace stats.
 set -o pipefail
 TAG=${1:-r04d}
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp; cd $R

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round 4, first session on the cost-residual build: new tests, full GPU suite,
-# same-box A/B (round-3 library vs this build with the residual on / off),
-# PMC traffic (FETCH_SIZE / WRITE_SIZE passes), bench, kernel-trace stats.
+# Round 4 session on the cost-residual build: SAD-family rate ubench, new tests,
+# full GPU suite, same-box A/B (round-3 library vs this build, lines on / off the
+# aux stream), PMC traffic (FETCH_SIZE / WRITE_SIZE passes), bench, kernel-trace
+# stats, config-5 frame probe, batches-in-flight sweep.  Usage: bash tools/gpu_r04e.sh TAG
 set -o pipefail
 TAG=${1:-r04e}
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp; cd $R
