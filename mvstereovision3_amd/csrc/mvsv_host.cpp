@@ -459,7 +459,9 @@ size_t mvsv_sgbm_workspace_bytes(int n, int W, int H, const mvsv_sgbm_params* p)
     size_t frame = (size_t)W * H;
     size_t vol = e.W1 > 0 ? (size_t)e.W1 * H * e.D * 2 : 0;
     size_t b = (size_t)n * (frame * 4 + 2 * vol + frame * 2);
-    if (e.speckle_window > 0) b += (size_t)n * frame * 8;
+    // speckle filter (speckle_buffers, mvsv_post.hip): parent, size and tile
+    // words, u16 local roots and the compact root list (+ its count)
+    if (e.speckle_window > 0) b += (size_t)n * frame * (4 + 4 + 4 + 2 + 4) + 4;
     // cost residual plane + per-pixel minimum (MVSV_OPT_COST_RESIDUAL, where exact)
     if (3 * e.P2 <= 15 && e.D <= 128 && e.W1 > 0) b += (size_t)n * e.W1 * H * (e.D / 2 + 2);
     return b;

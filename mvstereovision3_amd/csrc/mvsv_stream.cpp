@@ -46,9 +46,15 @@ static constexpr size_t kPoolMinBytes = (size_t)1 << 20;  // smaller copies stay
 // counter after run returns).
 class CopyPool {
   public:
+    // A worker that cannot be created (std::system_error, bad_alloc) leaves the
+    // pool with the workers made so far: nothing escapes into the C ABI.
     explicit CopyPool(int threads)
     {
-        for (int i = 1; i < threads; i++) workers_.emplace_back([this] { loop(); });
+        try {
+            workers_.reserve((size_t)std::max(threads - 1, 0));
+            for (int i = 1; i < threads; i++) workers_.emplace_back([this] { loop(); });
+        } catch (...) {
+        }
     }
     ~CopyPool()
     {
@@ -231,7 +237,13 @@ int mvsv_stream_create(mvsv_ctx* ctx, int W, int H, const mvsv_sgbm_params* p, i
     if (ok && px * 2 >= kPoolMinBytes) {
         int threads = 4;
         if (const char* v = std::getenv("MVSV_STREAM_COPY_THREADS")) threads = std::max(1, std::min(16, std::atoi(v)));
-        if (threads > 1) st->pool = new (std::nothrow) CopyPool(threads);
+        if (threads > 1) {
+            try {
+                st->pool = new CopyPool(threads);
+            } catch (...) {
+                st->pool = nullptr;  // copies on the caller's thread
+            }
+        }
     }
     if (!ok) {
         (void)hipGetLastError();

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -222,6 +223,11 @@ class DisparityStream:
                                        depth, ctypes.byref(roi) if roi is not None else None,
                                        ctypes.byref(h)), self._ctx.handle)
         self._h = h
+        # pinned host slots stay allocated while pop views are alive: a view's
+        # buffer references the stream, and close() defers the destroy until
+        # the last view is gone (use-after-free otherwise)
+        self._live_views = 0
+        self._close_pending = False
         if batch != 1:
             self.set_batch(batch)
         if inflight != 1:
@@ -242,7 +248,13 @@ class DisparityStream:
     def pending(self):
         return int(lib().mvsv_stream_pending(self._h))
 
+    def _live(self):
+        if self.closed:
+            raise MvsvError(_lib.MVSV_E_INVALID_ARG, "stream is closed")
+        return self._h
+
     def push(self, left, right):
+        self._live()
         L = np.asarray(left)
         R = np.asarray(right)
         if L.shape != (self.height, self.width) or R.shape != L.shape or L.dtype != np.uint8 \
@@ -259,6 +271,7 @@ class DisparityStream:
         """(map, means) of the oldest frame; copy_map=False returns (None, means);
         copy_map="view" returns a read-only view of the map in the stream's pinned
         host slot (no host copy), valid until the next push."""
+        self._live()
         if copy_map == "view":
             ptr = ctypes.c_void_p()
             means = np.empty(81, np.float32) if self._grid else None
@@ -266,6 +279,9 @@ class DisparityStream:
                                              means.ctypes.data if means is not None else None),
                   self._ctx.handle)
             buf = (ctypes.c_int16 * (self.width * self.height)).from_address(ptr.value)
+            buf._owner = self  # numpy's base chain keeps the stream (and its slots) alive
+            self._live_views += 1
+            weakref.finalize(buf, DisparityStream._view_released, self)
             view = np.ctypeslib.as_array(buf).reshape(self.height, self.width)
             view.flags.writeable = False
             return view, means
@@ -276,10 +292,28 @@ class DisparityStream:
               self._ctx.handle)
         return out, means
 
-    def close(self):
+    @staticmethod
+    def _view_released(stream):
+        stream._live_views -= 1
+        if stream._close_pending and stream._live_views == 0:
+            stream._destroy()
+
+    def _destroy(self):
         if self._h:
             lib().mvsv_stream_destroy(self._h)
             self._h = None
+        self._close_pending = False
+
+    def close(self):
+        """Destroys the stream; with pop views still alive, when the last one goes."""
+        if self._live_views > 0:
+            self._close_pending = True
+            return
+        self._destroy()
+
+    @property
+    def closed(self):
+        return self._h is None or self._close_pending
 
     def __del__(self):  # pragma: no cover
         try:

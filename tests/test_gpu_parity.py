@@ -585,3 +585,27 @@ def test_stream_copy_pool_and_pop_view(gpu, mvsv, oracle, threads, monkeypatch):
         if i % 2:
             assert np.array_equal(got[i][1], got[i][0])
     st.close()
+
+
+def test_stream_pop_view_outlives_close(gpu, mvsv):
+    """A pop view keeps the stream's pinned slot alive: close() and
+    dropping the stream while the view exists defer the destroy; the view still
+    reads the frame's map, and the stream refuses push / pop once closed."""
+    W, H, D = 320, 96, 32
+    m = mvsv.StereoSGBM.create(0, D, 5, 8 * 25, 32 * 25)
+    st = mvsv.DisparityStream(m, W, H, depth=2)
+    L, R = mvsv.synth_pair(SEED0 + 97, W, H, 0, D)
+    st.push(L, R)
+    view, _ = st.pop(copy_map="view")
+    want = m.compute(L, R)
+    st.close()
+    assert st.closed
+    with pytest.raises(mvsv.MvsvError):
+        st.push(L, R)
+    del st
+    import gc
+
+    gc.collect()
+    assert np.array_equal(view, want)
+    del view
+    gc.collect()

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of environment-selected kernel variants on the bench workload (same box,
 # alternating runs).  Usage (on the box): bash tools/ab_env.sh TAG ROUNDS "ENV_A" "ENV_B" [bench args]
-# e.g. bash tools/ab_env.sh ab1 3 "" "MVSV_STRIP_LPC=8"
+# e.g. bash tools/ab_env.sh ab1 3 "" "MVSV_STRIP_WAVES=8"
 set -o pipefail
 T=$1; N=$2; A=$3; B=$4; shift 4
 cd $GRAFT_REPO_ROOT

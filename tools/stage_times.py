@@ -3,7 +3,7 @@
 Usage (on the GPU box): python tools/stage_times.py [--frames F] [--width W --height H]
     [--ndisp D] [--mode 0|1] [--p1 P1 --p2 P2 --bs BS] [--steps K]
 Defaults: config 5 (liveDisparity: create(0, 256, 9, 648, 2592), MODE_SGBM, one
-1280x960 frame).  Env knobs (MVSV_STRIP_LPC, MVSV_PATH_SCHEDULE, ...) apply."""
+1280x960 frame).  Env knobs (MVSV_PATH_SCHEDULE, MVSV_STRIP_WAVES, ...) apply."""
 import argparse
 import json
 import os
