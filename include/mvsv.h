@@ -117,7 +117,12 @@ enum {
      * than C) instead of C where that is exact: no int16 wrap is possible,
      * 3*P2 <= 15 and numDisparities <= 128 (configs/sgbm.yml).  1 (default)
      * = on, 0 = always read C (A/B runs); results are identical either way. */
-    MVSV_OPT_COST_RESIDUAL = 6
+    MVSV_OPT_COST_RESIDUAL = 6,
+    /* Bit-sliced MODE_HH path aggregation (round 5, mvsv_bsgm.hip): 1 (default)
+     * = where it applies (MODE_HH, numDisparities 128, P1 2 / P2 5 -- the
+     * sgbm.yml regime --, uniquenessRatio 0, no int16 wrap); 0 = the packed
+     * int16 kernels.  Results are identical either way. */
+    MVSV_OPT_BITSLICE = 7
 };
 
 /* StereoSGBM modes (cv::StereoSGBM::MODE_SGBM / MODE_HH). */

@@ -6,7 +6,7 @@ src/disparity.cpp:6-108).  Compute lives in hand-written HIP kernels for
 gfx950 behind the C ABI of libmvsv.so (include/mvsv.h); this package is the
 host-side mirror of the reference interface.
 """
-from ._lib import (MODE_HH, MODE_SGBM, MVSV_E_TIMEOUT, OPT_BM_TILE_ROWS, OPT_PATH_SCHEDULE,
+from ._lib import (MODE_HH, MODE_SGBM, MVSV_E_TIMEOUT, OPT_BITSLICE, OPT_BM_TILE_ROWS, OPT_PATH_SCHEDULE,
                    OPT_STRIP_SPIN_LIMIT, OPT_STRIP_WAVES,
                    PREFILTER_NORMALIZED_RESPONSE, PREFILTER_XSOBEL, VARIANT_FIRSTCOL_FIX,
                    VARIANT_WTA_MIN_D, MvsvError, set_option, synchronize)
@@ -25,6 +25,6 @@ __all__ = [
     "dMapValues", "ply", "reproject", "init_undistort_rectify_map", "rectify_pair", "remap",
     "synchronize", "set_option", "Stereosystem", "read_matrix", "write_matrices",
     "stereo_rectify", "MVSV_E_TIMEOUT", "OPT_STRIP_SPIN_LIMIT", "OPT_STRIP_WAVES", "OPT_BM_TILE_ROWS",
-    "OPT_PATH_SCHEDULE",
+    "OPT_PATH_SCHEDULE", "OPT_BITSLICE",
 ]
 __version__ = "1.0.0"

@@ -31,6 +31,7 @@ OPT_STRIP_WAVES = 3
 OPT_PATH_SCHEDULE = 4
 OPT_STRIP_TICKETS = 5
 OPT_COST_RESIDUAL = 6
+OPT_BITSLICE = 7
 
 MODE_SGBM = 0
 MODE_HH = 1

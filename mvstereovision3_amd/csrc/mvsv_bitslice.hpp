@@ -1,0 +1,197 @@
+// mvsv_bitslice.hpp — bit-sliced SGM arithmetic (round 5).
+//
+// In the headline regime (configs/sgbm.yml: P1 = 2, P2 = 5 after OpenCV's
+// defaulting, the no-wrap bound) every quantity a direction pass
+// carries is a small integer: the clamped cost residual C' = min(C - min_d C,
+// 2 P2) <= 10, the path state s(d) = min(L(d) - min_d L, P2) <= 5 and the
+// delta = min(s(d), s(d -+ 1) + P1, P2) <= 5 (the
+// residual's exactness argument is DESIGN.md §4b).  So the passes run
+// bit-sliced: one 32-bit word holds bit b of 32 disparities, a 3-input
+// boolean function of three such words is one v_bitop3_b32, and a lane
+// updates 32 disparities of one bit plane per instruction instead of two
+// (packed int16).  Disparity order inside a pixel's 64-disparity half h:
+// word (h, e, b) bit p <-> d = 64 h + 2 p + e (E = even-d word, O = odd-d word).
+//
+// These helpers are per lane and per word and compile for the host too (the
+// CPU check tests/cpp/bitslice_check.cpp runs the same functions against a
+// scalar recurrence); the cross-lane steps live in the kernels.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define MVSV_BS_HD __host__ __device__ __forceinline__
+#else
+#define MVSV_BS_HD inline
+#endif
+
+namespace mvsv {
+namespace bs {
+
+// truth-table operands of v_bitop3_b32: result bit = TT[(a << 2) | (b << 1) | c]
+constexpr unsigned kA = 0xF0u, kB = 0xCCu, kC = 0xAAu;
+
+template <unsigned TT>
+MVSV_BS_HD uint32_t lop3(uint32_t a, uint32_t b, uint32_t c)
+{
+    static_assert(TT < 256u, "3-input truth table");
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
+#else
+    uint32_t r = 0;
+    for (int i = 0; i < 8; i++)
+        if (TT & (1u << i)) r |= ((i & 4) ? a : ~a) & ((i & 2) ? b : ~b) & ((i & 1) ? c : ~c);
+    return r;
+#endif
+}
+
+// {hi:lo} >> s (v_alignbit_b32), 0 <= s < 32
+MVSV_BS_HD uint32_t fshr(uint32_t hi, uint32_t lo, unsigned s)
+{
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> s);
+}
+
+// truth tables used below
+constexpr unsigned kAndNotAB = (~kA & kB) & 0xFFu;                  // ~a & b
+constexpr unsigned kLtChain = ((~kA & kB) | (~(kA ^ kB) & kC)) & 0xFFu;  // [a < b] with carry-in c; also the borrow of a - b - c
+constexpr unsigned kMux = ((kA & kB) | (~kA & kC)) & 0xFFu;        // a ? b : c
+constexpr unsigned kXor3 = (kA ^ kB ^ kC) & 0xFFu;
+constexpr unsigned kMaj = ((kA & kB) | (kA & kC) | (kB & kC)) & 0xFFu;
+static_assert(kAndNotAB == 0x0C && kLtChain == 0x8E && kMux == 0xCA && kXor3 == 0x96 && kMaj == 0xE8,
+              "bitop3 truth tables");
+
+// r = min(a, b) of two 3-bit sliced values (6 instructions)
+MVSV_BS_HD void min3b(const uint32_t (&a)[3], const uint32_t (&b)[3], uint32_t (&r)[3])
+{
+    const uint32_t l0 = lop3<kAndNotAB>(a[0], b[0], a[0]);
+    const uint32_t l1 = lop3<kLtChain>(a[1], b[1], l0);
+    const uint32_t lt = lop3<kLtChain>(a[2], b[2], l1);  // a < b
+    r[0] = lop3<kMux>(lt, a[0], b[0]);
+    r[1] = lop3<kMux>(lt, a[1], b[1]);
+    r[2] = lop3<kMux>(lt, a[2], b[2]);
+}
+
+// truth table of output bit k of u = min(t + P1, P2) over the 3-bit t (all 8
+// codes: a neighbour outside [0, D) is the code 7 and maps to P2)
+template <int P1, int P2>
+constexpr unsigned g_table(int k)
+{
+    unsigned tt = 0;
+    for (int t = 0; t < 8; t++) {
+        const int u = t + P1 < P2 ? t + P1 : P2;
+        if ((u >> k) & 1) tt |= 1u << t;
+    }
+    return tt;
+}
+template <int P1, int P2>
+MVSV_BS_HD void gmap(const uint32_t (&t)[3], uint32_t (&u)[3])
+{
+    u[0] = lop3<g_table<P1, P2>(0)>(t[2], t[1], t[0]);
+    u[1] = lop3<g_table<P1, P2>(1)>(t[2], t[1], t[0]);
+    u[2] = lop3<g_table<P1, P2>(2)>(t[2], t[1], t[0]);
+}
+
+// the path delta of one word: min(s, min(s(d-1), s(d+1)) + P1, P2) with the
+// neighbour words sl / sr already aligned to s (15 instructions)
+template <int P1, int P2>
+MVSV_BS_HD void delta3(const uint32_t (&s)[3], const uint32_t (&sl)[3],
+                                                const uint32_t (&sr)[3], uint32_t (&dl)[3])
+{
+    uint32_t t[3], u[3];
+    min3b(sl, sr, t);
+    gmap<P1, P2>(t, u);
+    min3b(s, u, dl);
+}
+
+// v = c + d, c 4-bit, d 3-bit, the sum known to be <= 15 (7 instructions)
+MVSV_BS_HD void add43(const uint32_t (&c)[4], const uint32_t (&d)[3], uint32_t (&v)[4])
+{
+    const uint32_t k0 = c[0] & d[0];
+    v[0] = c[0] ^ d[0];
+    v[1] = lop3<kXor3>(c[1], d[1], k0);
+    const uint32_t k1 = lop3<kMaj>(c[1], d[1], k0);
+    v[2] = lop3<kXor3>(c[2], d[2], k1);
+    const uint32_t k2 = lop3<kMaj>(c[2], d[2], k1);
+    v[3] = c[3] ^ k2;
+}
+
+// v = a + b, both 3-bit, 4-bit result (6 instructions)
+MVSV_BS_HD void add33(const uint32_t (&a)[3], const uint32_t (&b)[3], uint32_t (&v)[4])
+{
+    const uint32_t k0 = a[0] & b[0];
+    v[0] = a[0] ^ b[0];
+    v[1] = lop3<kXor3>(a[1], b[1], k0);
+    const uint32_t k1 = lop3<kMaj>(a[1], b[1], k0);
+    v[2] = lop3<kXor3>(a[2], b[2], k1);
+    v[3] = lop3<kMaj>(a[2], b[2], k1);
+}
+
+// v = a + b, both 4-bit, 5-bit result (8 instructions)
+MVSV_BS_HD void add44(const uint32_t (&a)[4], const uint32_t (&b)[4], uint32_t (&v)[5])
+{
+    const uint32_t k0 = a[0] & b[0];
+    v[0] = a[0] ^ b[0];
+    v[1] = lop3<kXor3>(a[1], b[1], k0);
+    const uint32_t k1 = lop3<kMaj>(a[1], b[1], k0);
+    v[2] = lop3<kXor3>(a[2], b[2], k1);
+    const uint32_t k2 = lop3<kMaj>(a[2], b[2], k1);
+    v[3] = lop3<kXor3>(a[3], b[3], k2);
+    v[4] = lop3<kMaj>(a[3], b[3], k2);
+}
+
+// v = a + b, a 5-bit, b 4-bit, the sum known to be < 64 (6-bit result, 9 instructions)
+MVSV_BS_HD void add54(const uint32_t (&a)[5], const uint32_t (&b)[4], uint32_t (&v)[6])
+{
+    const uint32_t k0 = a[0] & b[0];
+    v[0] = a[0] ^ b[0];
+    v[1] = lop3<kXor3>(a[1], b[1], k0);
+    const uint32_t k1 = lop3<kMaj>(a[1], b[1], k0);
+    v[2] = lop3<kXor3>(a[2], b[2], k1);
+    const uint32_t k2 = lop3<kMaj>(a[2], b[2], k1);
+    v[3] = lop3<kXor3>(a[3], b[3], k2);
+    const uint32_t k3 = lop3<kMaj>(a[3], b[3], k2);
+    v[4] = a[4] ^ k3;
+    v[5] = a[4] & k3;
+}
+
+// s = min(v - m, P2) for a 4-bit v >= m and a lane-uniform 3-bit m given as
+// all-ones / all-zero masks m0..m2 (13 instructions)
+template <int P2>
+MVSV_BS_HD void subclamp(const uint32_t (&v)[4], uint32_t m0, uint32_t m1, uint32_t m2,
+                                                  uint32_t (&s)[3])
+{
+    static_assert(P2 >= 2 && P2 <= 5, "3-bit states: P2 in [2, 5]");
+    const uint32_t r0 = v[0] ^ m0;
+    const uint32_t b0 = lop3<kAndNotAB>(v[0], m0, m0);
+    const uint32_t r1 = lop3<kXor3>(v[1], m1, b0);
+    const uint32_t b1 = lop3<kLtChain>(v[1], m1, b0);
+    const uint32_t r2 = lop3<kXor3>(v[2], m2, b1);
+    const uint32_t b2 = lop3<kLtChain>(v[2], m2, b1);
+    // r3 = v3 ^ b2; ge = [r >= P2] = r3 | y
+    uint32_t y;
+    if constexpr (P2 == 2)
+        y = r2 | r1;
+    else if constexpr (P2 == 3)
+        y = lop3<(kA | (kB & kC)) & 0xFFu>(r2, r1, r0);
+    else if constexpr (P2 == 4)
+        y = r2;
+    else
+        y = lop3<(kA & (kB | kC)) & 0xFFu>(r2, r1, r0);
+    const uint32_t ge = lop3<((kA ^ kB) | kC) & 0xFFu>(v[3], b2, y);
+    s[0] = (P2 & 1) ? (r0 | ge) : lop3<(kA & ~kB) & 0xFFu>(r0, ge, ge);
+    s[1] = (P2 & 2) ? (r1 | ge) : lop3<(kA & ~kB) & 0xFFu>(r1, ge, ge);
+    s[2] = (P2 & 4) ? (r2 | ge) : lop3<(kA & ~kB) & 0xFFu>(r2, ge, ge);
+}
+
+// scalar value of a sliced number at word bit p (host checks, sub-pixel reads)
+template <int NB>
+MVSV_BS_HD int bits_at(const uint32_t (&w)[NB], int p)
+{
+    int v = 0;
+    for (int k = 0; k < NB; k++) v |= (int)((w[k] >> p) & 1u) << k;
+    return v;
+}
+
+}  // namespace bs
+}  // namespace mvsv

@@ -1,0 +1,778 @@
+// mvsv_bsgm.hip — bit-sliced MODE_HH path aggregation (round 5).
+//
+// The same eight SGM directions as the packed-int16 kernels of mvsv_sgbm.hip
+// (OpenCV 3.4 computeDisparitySGBM, reached through Disparity::sgbm /
+// loadSGBMParameters, /root/reference/src/disparity.cpp:6-10,92-95; semantics in
+// SURVEY.md Appendix A.4-A.5), restated on bit planes (mvsv_bitslice.hpp): in
+// the headline regime (P1 = 2, P2 = 5, no-wrap, D = 128, uniquenessRatio 0)
+// a direction's state s(d) = min(L(d) - min L, P2), its delta and the clamped
+// cost residual C' are 3- and 4-bit numbers, so one v_bitop3_b32 updates 32
+// disparities of one bit.  A pixel's 128 disparities live on two lanes (h = 0,
+// 1: d in [64 h, 64 h + 64)) as parity words E (even d) / O (odd d), one per
+// bit; d -+ 1 neighbours are the other parity word, shifted by one where the
+// pair crosses into the partner lane (one DPP swap).
+//
+//   bsgm_strip_kernel  the six vertical / diagonal directions of both passes on
+//                      sheared strips (the strip chain, tickets and boundary
+//                      hand-off of sgbm_tri_kernel), one wave per direction
+//   bsgm_lines_kernel  L->R and R->L along the rows
+//   bsgm_wta_kernel    S'' = 8 C' + sum of deltas, argmin (smallest d), exact
+//                      S(best -+ 1) for the parabola, right-view keys, LR check
+//
+// Data (per frame, W1 cost columns): C' planes and each strip pass's delta-sum
+// planes [H][W1][16 words] (64 B per pixel: word h*8 + e*4 + b); line delta
+// planes [H][W1][12 words] (h*6 + e*3 + b).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <type_traits>
+#include <vector>
+
+#include "mvsv_bitslice.hpp"
+#include "mvsv_device.hpp"
+#include "mvsv_internal.hpp"
+
+namespace mvsv {
+
+using namespace dev;
+
+namespace {
+
+constexpr uint32_t kOnes = 0xffffffffu;
+
+// value of the partner lane (lane ^ 1: the pixel's other 64-disparity half)
+__device__ __forceinline__ uint32_t xswap(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true);  // quad_perm [1,0,3,2]
+}
+
+// One direction step of one pixel on its lane pair (mirrored on the host by
+// pair_step in tests/cpp/bitslice_check.cpp).  s: previous state (E / O words
+// of 3 bits), c: C' of the cell (4 bits); fill0 / fill1 = all-ones on the h = 0
+// / h = 1 lane (disparities -1 and 128 read the code 7, which maps to P2).
+// Out: the new state n and the delta d.
+template <int P1, int P2>
+__device__ __forceinline__ void bs_dir_step(const uint32_t (&sE)[3], const uint32_t (&sO)[3],
+                                            const uint32_t (&cE)[4], const uint32_t (&cO)[4], uint32_t fill0,
+                                            uint32_t fill1, uint32_t (&nE)[3], uint32_t (&nO)[3],
+                                            uint32_t (&dE)[3], uint32_t (&dO)[3])
+{
+    uint32_t slE[3], srO[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint32_t prevO = xswap(sO[k]) | fill0;  // d = 64 h - 1: the h = 0 lane's last odd word
+        const uint32_t nextE = xswap(sE[k]) | fill1;  // d = 64 h + 64: the h = 1 lane's first even word
+        slE[k] = bs::fshr(sO[k], prevO, 31);
+        srO[k] = bs::fshr(nextE, sE[k], 1);
+    }
+    bs::delta3<P1, P2>(sE, slE, sO, dE);
+    bs::delta3<P1, P2>(sO, sE, srO, dO);
+    uint32_t vE[4], vO[4];
+    bs::add43(cE, dE, vE);
+    bs::add43(cO, dO, vO);
+    // min over the pixel's 128 v = C' + delta, bit-serial from bit 2: some d has
+    // C' = 0, so the minimum is <= P2 < 8
+    uint32_t kE = ~vE[3], kO = ~vO[3], M[3];
+#pragma unroll
+    for (int b = 2; b >= 0; b--) {
+        const uint32_t zE = bs::lop3<bs::kAndNotAB>(vE[b], kE, kE);
+        const uint32_t zO = bs::lop3<bs::kAndNotAB>(vO[b], kO, kO);
+        uint32_t any = zE | zO;
+        any |= xswap(any);
+        const bool f = any != 0u;
+        if (b > 0) {
+            kE = f ? zE : kE;
+            kO = f ? zO : kO;
+        }
+        M[b] = f ? 0u : kOnes;
+    }
+    bs::subclamp<P2>(vE, M[0], M[1], M[2], nE);
+    bs::subclamp<P2>(vO, M[0], M[1], M[2], nO);
+}
+
+// ---------------------------------------------------------------------------
+// Strips: the three directions of a pass on sheared U-columns (U = x - t + H - 1,
+// t the step: y for the down pass, H - 1 - y for the up pass); the
+// predecessors of U at step t are U (dir a = (1, sy)), U + 1 (b = (0, sy)) and
+// U + 2 (c = (-1, sy)) of step t - 1 (the geometry of sgbm_tri_kernel).  A block
+// owns 32 NG U-columns; wave 3 g + r runs direction r for columns 32 g .. 32 g +
+// 31 of the strip (two lanes per column), the last wave moves the strip's
+// boundary states to / from its neighbours.  Directions b and c hand their
+// new states and deltas over through LDS; wave a sums the three deltas of a
+// cell one step later and stores the pass's 4-bit plane.
+// ---------------------------------------------------------------------------
+template <int NG>
+struct BsStripCfg {
+    static constexpr int kSW = 32 * NG;          // U-columns per strip
+    static constexpr int kCompute = 3 * NG;      // compute waves
+    static constexpr int kThreads = 64 * (kCompute + 1);
+    static constexpr int kCols = kSW + 2;        // + two columns of the right strip
+    static constexpr int kSt = 2 * 2 * 6 * kCols * 2;  // states [buf][dir b, c][word][col][h]
+    static constexpr int kDl = 2 * 2 * 6 * kSW * 2;    // deltas [buf][dir b, c][word][col][h]
+    static constexpr size_t kBytes = (size_t)(kSt + kDl) * 4;
+};
+// boundary words per strip step: (dir b, column 0), (dir c, column 0), (dir c,
+// column 1), each 2 lanes x 6 words; one u64 granule = 32-bit launch tag | word
+constexpr int kBsGran = 36;
+constexpr int kBsPF = 4;  // steps of C' prefetch (compute waves)
+constexpr int kBsBF = 4;  // steps of boundary prefetch (exchange wave)
+
+template <int NG, int P1, int P2>
+__global__ __launch_bounds__(BsStripCfg<NG>::kThreads) void bsgm_strip_kernel(
+    const uint32_t* __restrict__ Bc, uint32_t* __restrict__ A, size_t plane_words, uint32_t* __restrict__ dummy,
+    int H, int W1, int npass,
+    unsigned long long* __restrict__ bnd, unsigned epoch, int nframes, int* __restrict__ status,
+    unsigned spin_limit, int* __restrict__ report, long long ticket0, unsigned long long* __restrict__ stats,
+    int nowait)
+{
+    using Cfg = BsStripCfg<NG>;
+    constexpr int SW = Cfg::kSW, NCOL = Cfg::kCols;
+    extern __shared__ __attribute__((aligned(16))) uint32_t bs_lds[];
+    uint32_t* st = bs_lds;
+    uint32_t* dlt = bs_lds + Cfg::kSt;
+    auto sti = [&](int buf, int d, int k, int c, int h) { return (((buf * 2 + d) * 6 + k) * NCOL + c) * 2 + h; };
+    auto dli = [&](int buf, int d, int k, int c, int h) { return (((buf * 2 + d) * 6 + k) * SW + c) * 2 + h; };
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool comm = w == Cfg::kCompute;
+
+    // strip ticket (sgbm_tri_kernel: a strip only ever waits on a strip whose
+    // block arrived before it, whatever the dispatch order)
+    __shared__ int s_ticket;
+    if (threadIdx.x == 0)
+        s_ticket = ticket0 < 0 ? (int)blockIdx.x
+                               : (int)(__hip_atomic_fetch_add((unsigned*)status + 2, 1u, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT) - (unsigned)ticket0);
+    __syncthreads();
+    const int bx = s_ticket;
+    if ((unsigned)bx >= gridDim.x) {
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(status, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(report, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
+    const int nchains = npass * nframes;
+    const int k = bx / nchains;
+    const int chain = bx - k * nchains;
+    const int pass = chain / nframes;
+    const int f = chain - pass * nframes;
+    const int sy = pass == 0 ? 1 : -1;
+    const int Utot = W1 + H - 1;
+    const int U0 = Utot - SW * (k + 1);
+    const int tb = max(0, (H - 1) - (U0 + SW - 1));
+    const int te = min(H, W1 + (H - 1) - U0);
+    if (tb >= te) return;
+
+    for (int i = threadIdx.x; i < Cfg::kSt + Cfg::kDl; i += Cfg::kThreads) bs_lds[i] = 0u;
+
+    // ---- exchange wave: lane j < 36 carries word (h, k) = (j % 12 / 6, j % 6)
+    // of item j / 12; lanes 36..63 repeat lanes 0..27 (same addresses, same
+    // values), so every memory instruction is unpredicated
+    const int jj = lane < kBsGran ? lane : lane - kBsGran;
+    const int item = jj / 12, wi = jj - 12 * item;
+    const int ih = wi / 6, ik = wi - 6 * ih;
+    const int idir = item == 0 ? 0 : 1;
+    const int icol_in = SW + (item == 2 ? 1 : 0);  // LDS column the right strip's item lands in
+    const int icol_out = item == 2 ? 1 : 0;        // own column published as item
+    const size_t slot_step = kBsGran;
+    const unsigned long long* bsrc =
+        bnd + (((size_t)(k > 0 ? k - 1 : 0) * nchains + chain) * H) * slot_step + jj;
+    unsigned long long* pdst = bnd + (((size_t)k * nchains + chain) * H) * slot_step + jj;
+    const unsigned long long tag = (unsigned long long)epoch << 32;
+    auto bvalid = [&](int t) {
+        const int xx = U0 + icol_in - (H - 1) + t;
+        return k > 0 && t >= 0 && xx >= 0 && xx < W1;
+    };
+    auto bload = [&](int t) -> unsigned long long {
+        return __hip_atomic_load(bsrc + (size_t)clampi(t, 0, H - 1) * slot_step, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    };
+    unsigned long long st_t0 = stats ? __builtin_amdgcn_s_memtime() : 0ull, st_spin = 0, st_n = 0;
+    auto bconsume = [&](int t, int buf, unsigned long long g) {
+        const bool need = bvalid(t);
+        bool ok = nowait || !need || (unsigned)(g >> 32) == epoch;
+        if (!__all(ok)) {
+            const unsigned long long sp0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+            unsigned spins = 0;
+            while (!__all(ok)) {
+                if (++spins > spin_limit) {
+                    if (lane == 0) {
+                        __hip_atomic_store(status, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(report, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                    break;
+                }
+                if ((spins & 63) == 0 &&
+                    __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)epoch)
+                    break;
+                __builtin_amdgcn_s_sleep(1);
+                g = bload(t);
+                ok = !need || (unsigned)(g >> 32) == epoch;
+            }
+            if (stats) {
+                st_spin += __builtin_amdgcn_s_memtime() - sp0;
+                st_n += spins;
+            }
+        }
+        st[sti(buf, idir, ik, icol_in, ih)] = need ? (uint32_t)g : 0u;
+    };
+    auto publish = [&](int t, int buf) {
+        const uint32_t v = st[sti(buf, idir, ik, icol_out, ih)];
+        __hip_atomic_store(pdst + (size_t)clampi(t, 0, H - 1) * slot_step, tag | v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    };
+
+    // ---- compute waves
+    const int grp = comm ? 0 : w / 3;
+    const int dir = comm ? 0 : w - 3 * grp;  // 0 = (1, sy), 1 = (0, sy), 2 = (-1, sy)
+    const int u = lane >> 1, h = lane & 1;
+    const int col = grp * 32 + u;
+    const int U = U0 + col;
+    const uint32_t fill0 = h == 0 ? kOnes : 0u, fill1 = h == 1 ? kOnes : 0u;
+    auto cell_x = [&](int t) { return U - (H - 1) + t; };
+    // word offset of the lane's half of cell (x(t), y(t)); cells outside the
+    // image read the frame's first cell (their results are discarded)
+    const int rowW = sy > 0 ? W1 : -W1;
+    const int c0 = ((f * H + (sy > 0 ? 0 : H - 1)) * W1 + U - (H - 1)) * 16 + h * 8;
+    const int cst = (rowW + 1) * 16;
+    const int fbase = f * H * W1 * 16 + h * 8;
+    auto cell_off = [&](int t) -> int { return (unsigned)cell_x(t) < (unsigned)W1 ? c0 + t * cst : fbase; };
+    uint32_t* Ap = A + (size_t)pass * plane_words;
+    uint4 cb[kBsPF][2];
+    uint32_t sa[6];  // direction a's state (E words 0..2, O words 3..5)
+#pragma unroll
+    for (int q = 0; q < 6; q++) sa[q] = 0u;
+    uint32_t pdl[6];  // direction a's delta of the previous step
+    int pend_off = -1;
+    unsigned long long bg[kBsBF];
+
+    __syncthreads();  // LDS zeroed
+    if (comm) {
+        __builtin_amdgcn_s_setprio(1);  // the exchange wave gates every step's barrier
+        bconsume(tb - 1, 1, bload(tb - 1));
+#pragma unroll
+        for (int j = 0; j < kBsBF; j++) bg[j] = bload(tb + j);
+    } else {
+#pragma unroll
+        for (int j = 0; j < kBsPF; j++) {
+            const uint4* q = (const uint4*)(Bc + cell_off(min(tb + j, te - 1)));
+            cb[j][0] = q[0];
+            cb[j][1] = q[1];
+        }
+    }
+    __syncthreads();
+
+    auto comm_step = [&](int i, int j) {
+        const int t = tb + i;
+        const int cur = i & 1, prv = cur ^ 1;
+        if (i > 0) publish(t - 1, prv);
+        bconsume(t, cur, bg[j]);
+        bg[j] = bload(t + kBsBF);
+        __syncthreads();
+    };
+    // direction a: the three deltas of the previous step's cell -> the pass plane
+    auto flush_a = [&](int prv) {
+        uint32_t db[6], dc[6];
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+            db[q] = dlt[dli(prv, 0, q, col, h)];
+            dc[q] = dlt[dli(prv, 1, q, col, h)];
+        }
+        uint32_t o[2][4];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const uint32_t a3[3] = {pdl[3 * e], pdl[3 * e + 1], pdl[3 * e + 2]};
+            const uint32_t b3[3] = {db[3 * e], db[3 * e + 1], db[3 * e + 2]};
+            const uint32_t c3[3] = {dc[3 * e], dc[3 * e + 1], dc[3 * e + 2]};
+            uint32_t ab[4];
+            bs::add33(a3, b3, ab);
+            bs::add43(ab, c3, o[e]);  // <= 3 P2 = 15
+        }
+        // unpredicated: a cell outside the image stores into the lane's dummy
+        // slot, so the prefetch loads' wait counts stay exact
+        uint4* q = pend_off >= 0 ? (uint4*)(Ap + pend_off) : (uint4*)(dummy + lane * 8);
+        q[0] = make_uint4(o[0][0], o[0][1], o[0][2], o[0][3]);
+        q[1] = make_uint4(o[1][0], o[1][1], o[1][2], o[1][3]);
+    };
+    // one step of direction DIR (compile time: each direction's loop has its
+    // own LDS offsets and register allocation)
+    auto step = [&](auto dtag, int i, int j) {
+        constexpr int DIR = decltype(dtag)::value;
+        const int t = tb + i;
+        const int cur = i & 1, prv = cur ^ 1;
+        const int x = cell_x(t);
+        const bool valid = x >= 0 && x < W1;
+        const uint32_t cE[4] = {cb[j][0].x, cb[j][0].y, cb[j][0].z, cb[j][0].w};
+        const uint32_t cO[4] = {cb[j][1].x, cb[j][1].y, cb[j][1].z, cb[j][1].w};
+        uint32_t sE[3], sO[3];
+        if constexpr (DIR == 0) {
+            if (i > 0) flush_a(prv);
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                sE[q] = sa[q];
+                sO[q] = sa[3 + q];
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                sE[q] = st[sti(prv, DIR - 1, q, col + DIR, h)];
+                sO[q] = st[sti(prv, DIR - 1, 3 + q, col + DIR, h)];
+            }
+        }
+        uint32_t nE[3], nO[3], dE[3], dO[3];
+        bs_dir_step<P1, P2>(sE, sO, cE, cO, fill0, fill1, nE, nO, dE, dO);
+        {
+            // the slot's next load once its words are consumed (same registers)
+            const uint4* q = (const uint4*)(Bc + cell_off(min(t + kBsPF, te - 1)));
+            cb[j][0] = q[0];
+            cb[j][1] = q[1];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (!valid) {
+#pragma unroll
+            for (int q = 0; q < 3; q++) nE[q] = nO[q] = 0u;
+        }
+        if constexpr (DIR == 0) {
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                sa[q] = nE[q];
+                sa[3 + q] = nO[q];
+                pdl[q] = dE[q];
+                pdl[3 + q] = dO[q];
+            }
+            pend_off = valid ? cell_off(t) : -1;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                st[sti(cur, DIR - 1, q, col, h)] = nE[q];
+                st[sti(cur, DIR - 1, 3 + q, col, h)] = nO[q];
+                dlt[dli(cur, DIR - 1, q, col, h)] = dE[q];
+                dlt[dli(cur, DIR - 1, 3 + q, col, h)] = dO[q];
+            }
+        }
+        __syncthreads();
+    };
+    auto run = [&](auto dtag) {
+        const int len = te - tb;
+        int i = 0;
+        for (; i + kBsPF <= len; i += kBsPF) {
+#pragma unroll
+            for (int j = 0; j < kBsPF; j++) step(dtag, i + j, j);
+        }
+#pragma unroll
+        for (int j = 0; j < kBsPF; j++)
+            if (i + j < len) step(dtag, i + j, j);
+        __syncthreads();
+        if constexpr (decltype(dtag)::value == 0) flush_a((len - 1) & 1);
+    };
+    if (comm) {
+        const int len = te - tb;
+        int i = 0;
+        for (; i + kBsBF <= len; i += kBsBF) {
+#pragma unroll
+            for (int j = 0; j < kBsBF; j++) comm_step(i + j, j);
+        }
+#pragma unroll
+        for (int j = 0; j < kBsBF; j++)
+            if (i + j < len) comm_step(i + j, j);
+        __syncthreads();
+        publish(te - 1, (len - 1) & 1);
+        if (stats && lane == 0) {
+            unsigned long long* q = stats + (size_t)bx * 8;
+            q[0] = st_t0;
+            q[1] = __builtin_amdgcn_s_memtime();
+            q[2] = st_spin;
+            q[3] = st_n;
+            q[4] = (unsigned long long)len;
+            q[5] = (unsigned long long)k;
+            q[6] = (unsigned long long)pass;
+            q[7] = (unsigned long long)tb;
+        }
+    } else if (dir == 0) {
+        run(std::integral_constant<int, 0>());
+    } else if (dir == 1) {
+        run(std::integral_constant<int, 1>());
+    } else {
+        run(std::integral_constant<int, 2>());
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Lines: L->R (blockIdx.z = 0) and R->L (1), 32 rows per wave, two lanes per
+// row; each writes its delta plane (3 bits).
+// ---------------------------------------------------------------------------
+// One wave per block: 32 rows x 2 lanes.  The rows' C' records stream through
+// LDS in chunks of kBsChunk pixels -- each row's chunk is one contiguous
+// 512-byte run, loaded by whole-wave coalesced dwordx4 loads one chunk ahead
+// (registers -> padded LDS rows) -- because per-lane row loads (64 bytes from
+// each of 32 rows per step) measured 3x slower than the recurrence itself
+// (1.04 vs 0.33 ms for the 8-frame batch with every row reading one cached row).
+constexpr int kBsChunk = 8;
+constexpr int kBsLineRowB = kBsChunk * 64 + 16;  // LDS row stride (bytes): + 16 B against bank conflicts
+constexpr int kBsLineBufB = 32 * kBsLineRowB;
+
+template <int P1, int P2>
+__global__ __launch_bounds__(64) void bsgm_lines_kernel(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dl,
+                                                         size_t plane_words, int H, int W1, int probe)
+{
+    __shared__ __attribute__((aligned(16))) unsigned char lbuf[2 * kBsLineBufB];
+    const int lane = threadIdx.x;
+    const int h = lane & 1, rr = lane >> 1;
+    const int y0 = (int)blockIdx.x * 32;
+    const int y = min(y0 + rr, H - 1);
+    const int f = blockIdx.y;
+    const bool rl = blockIdx.z != 0;
+    const uint32_t fill0 = h == 0 ? kOnes : 0u, fill1 = h == 1 ? kOnes : 0u;
+    uint32_t* drow = Dl + (rl ? plane_words : 0) + ((size_t)(f * H + y) * W1) * 12 + h * 6;
+    // loader: instruction i covers rows 2 i + (lane >> 5), 16-byte piece lane & 31
+    // of the chunk's 512 bytes (pixel sg >> 2, piece sg & 3)
+    const int sg = lane & 31;
+    const uint32_t* lrow[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const int yy = probe ? 0 : min(y0 + 2 * i + (lane >> 5), H - 1);
+        lrow[i] = Bc + ((size_t)((probe ? 0 : f) * H + yy) * W1) * 16 + (sg & 3) * 4;
+    }
+    uint4 stg[16];
+    const int nch = (W1 + kBsChunk - 1) / kBsChunk;
+    auto chunk_base = [&](int c) { return rl ? W1 - kBsChunk * (c + 1) : kBsChunk * c; };
+    auto load_chunk = [&](int c) {
+        const int px = clampi(chunk_base(c) + (sg >> 2), 0, W1 - 1);
+#pragma unroll
+        for (int i = 0; i < 16; i++) stg[i] = *(const uint4*)(lrow[i] + (size_t)px * 16);
+    };
+    auto park_chunk = [&](int buf) {
+        unsigned char* b = lbuf + buf * kBsLineBufB + (lane >> 5) * kBsLineRowB + sg * 16;
+#pragma unroll
+        for (int i = 0; i < 16; i++) *(uint4*)(b + 2 * i * kBsLineRowB) = stg[i];
+    };
+    load_chunk(0);
+    park_chunk(0);
+    uint32_t sE[3] = {0u, 0u, 0u}, sO[3] = {0u, 0u, 0u};
+    const unsigned char* rbase = lbuf + rr * kBsLineRowB + h * 32;
+    for (int c = 0; c < nch; c++) {
+        if (c + 1 < nch) load_chunk(c + 1);
+        const unsigned char* cbuf = rbase + (c & 1) * kBsLineBufB;
+        const int b0 = chunk_base(c);
+#pragma unroll
+        for (int i = 0; i < kBsChunk; i++) {
+            const int st = kBsChunk * c + i;
+            if (st >= W1) break;
+            const int j = rl ? kBsChunk - 1 - i : i;
+            const uint4 e4 = *(const uint4*)(cbuf + j * 64), o4 = *(const uint4*)(cbuf + j * 64 + 16);
+            const uint32_t cE[4] = {e4.x, e4.y, e4.z, e4.w};
+            const uint32_t cO[4] = {o4.x, o4.y, o4.z, o4.w};
+            uint32_t nE[3], nO[3], dE[3], dO[3];
+            bs_dir_step<P1, P2>(sE, sO, cE, cO, fill0, fill1, nE, nO, dE, dO);
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                sE[q] = nE[q];
+                sO[q] = nO[q];
+            }
+            // unpredicated (lanes of rows past H repeat row H - 1: same values at
+            // the same addresses)
+            uint2* o = (uint2*)(drow + (size_t)(b0 + j) * 12);
+            o[0] = make_uint2(dE[0], dE[1]);
+            o[1] = make_uint2(dE[2], dO[0]);
+            o[2] = make_uint2(dO[1], dO[2]);
+        }
+        if (c + 1 < nch) park_chunk((c + 1) & 1);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// WTA: one block per image row.  S'' = 8 C' + A_down + A_up + d_LR + d_RL (7
+// bits; DESIGN.md §4b: same argmin and ties as S, exact minimum n (m - P2) +
+// min S''), argmin with the smallest d on ties (MODE_HH), S''(best -+ 1) read
+// off the bit planes, C(best -+ 1) gathered where the residual may be clamped,
+// parabola, right-view keys (order-independent atomicMin), then the row's LR
+// check (the final loop of OpenCV 3.4).
+// ---------------------------------------------------------------------------
+constexpr int kBsWtaThreads = 512;
+
+__global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t* __restrict__ Bc,
+                                                                 const uint32_t* __restrict__ A, size_t aplane,
+                                                                 const uint32_t* __restrict__ Dl, size_t dplane,
+                                                                 const int16_t* __restrict__ C,
+                                                                 const uint16_t* __restrict__ Mv, int H, int W,
+                                                                 SgbmEff e, int16_t* __restrict__ raw,
+                                                                 uint32_t* __restrict__ keys)
+{
+    constexpr int NDIR = 8;
+    const int y = blockIdx.x, f = blockIdx.y;
+    const int D = e.D, W1 = e.W1, minD = e.minD, minX1 = e.minX1;
+    const int INV = e.invalid;
+    int16_t* orow = raw + ((size_t)f * H + y) * W;
+    uint32_t* krow = keys + ((size_t)f * H + y) * W;
+    for (int x = threadIdx.x; x < W; x += kBsWtaThreads) {
+        orow[x] = (int16_t)INV;
+        krow[x] = 0xffffffffu;
+    }
+    __threadfence_block();
+    __syncthreads();
+    const int h = threadIdx.x & 1;
+    const size_t pix0 = ((size_t)f * H + y) * W1;
+    const int clampS = NDIR * 2 * e.P2;  // S'' >= this: C'' may be the clamp value
+    for (int xb = 0; xb < W1; xb += kBsWtaThreads / 2) {
+        const int xr = xb + (threadIdx.x >> 1);
+        const bool own = xr < W1;
+        const int x = min(xr, W1 - 1);
+        const size_t pix = pix0 + x;
+        uint32_t c[2][4], ad[2][4], au[2][4], dl[2][3], dr[2][3];
+        {
+            const uint4* qc = (const uint4*)(Bc + pix * 16 + h * 8);
+            const uint4* qd = (const uint4*)(A + pix * 16 + h * 8);
+            const uint4* qu = (const uint4*)(A + aplane + pix * 16 + h * 8);
+            const uint2* ql = (const uint2*)(Dl + pix * 12 + h * 6);
+            const uint2* qr = (const uint2*)(Dl + dplane + pix * 12 + h * 6);
+            uint4 t;
+#pragma unroll
+            for (int e2 = 0; e2 < 2; e2++) {
+                t = qc[e2];
+                c[e2][0] = t.x, c[e2][1] = t.y, c[e2][2] = t.z, c[e2][3] = t.w;
+                t = qd[e2];
+                ad[e2][0] = t.x, ad[e2][1] = t.y, ad[e2][2] = t.z, ad[e2][3] = t.w;
+                t = qu[e2];
+                au[e2][0] = t.x, au[e2][1] = t.y, au[e2][2] = t.z, au[e2][3] = t.w;
+            }
+            const uint2 l0 = ql[0], l1 = ql[1], l2 = ql[2];
+            const uint2 r0 = qr[0], r1 = qr[1], r2 = qr[2];
+            dl[0][0] = l0.x, dl[0][1] = l0.y, dl[0][2] = l1.x, dl[1][0] = l1.y, dl[1][1] = l2.x, dl[1][2] = l2.y;
+            dr[0][0] = r0.x, dr[0][1] = r0.y, dr[0][2] = r1.x, dr[1][0] = r1.y, dr[1][1] = r2.x, dr[1][2] = r2.y;
+        }
+        uint32_t S[2][7];
+#pragma unroll
+        for (int e2 = 0; e2 < 2; e2++) {
+            uint32_t s5[5], d4[4], s6[6], hi[4];
+            bs::add44(ad[e2], au[e2], s5);  // strips <= 2 * 3 P2 = 30
+            bs::add33(dl[e2], dr[e2], d4);  // lines <= 2 P2 = 10
+            bs::add54(s5, d4, s6);          // all deltas <= 8 P2 = 40
+            const uint32_t top[3] = {s6[3], s6[4], s6[5]};
+            bs::add43(c[e2], top, hi);      // 8 C' + deltas: high part <= 10 + 5
+            S[e2][0] = s6[0], S[e2][1] = s6[1], S[e2][2] = s6[2];
+            S[e2][3] = hi[0], S[e2][4] = hi[1], S[e2][5] = hi[2], S[e2][6] = hi[3];
+        }
+        // argmin: the minimum is <= 8 P2 = 40 < 64 (the d with C' = 0), so bit 6 is 0
+        uint32_t kE = ~S[0][6], kO = ~S[1][6];
+        int mins = 0;
+#pragma unroll
+        for (int b = 5; b >= 0; b--) {
+            const uint32_t zE = bs::lop3<bs::kAndNotAB>(S[0][b], kE, kE);
+            const uint32_t zO = bs::lop3<bs::kAndNotAB>(S[1][b], kO, kO);
+            uint32_t any = zE | zO;
+            any |= xswap(any);
+            const bool fz = any != 0u;
+            kE = fz ? zE : kE;
+            kO = fz ? zO : kO;
+            mins |= fz ? 0 : 1 << b;
+        }
+        // smallest d among the minima: the lower lane first, then the lowest bit
+        // position, even before odd
+        const uint32_t m = kE | kO;
+        const int p = __builtin_ctz(m | 0x80000000u);
+        const int mine = m ? 64 * h + 2 * p + (((kE >> p) & 1u) ? 0 : 1) : 1 << 20;
+        const int best = min(mine, (int)xswap((uint32_t)mine));
+        // S''(best -+ 1): both have the other parity; each lane reads its half
+        const int eb = best & 1;
+        int Sm = 0, Sp = 0;
+        {
+            const int pm = ((best - 1 - 64 * h) >> 1) & 31, pp = ((best + 1 - 64 * h) >> 1) & 31;
+#pragma unroll
+            for (int b = 0; b < 7; b++) {
+                const uint32_t wv = eb ? S[0][b] : S[1][b];
+                Sm |= (int)((wv >> pm) & 1u) << b;
+                Sp |= (int)((wv >> pp) & 1u) << b;
+            }
+            const int Smo = (int)xswap((uint32_t)Sm), Spo = (int)xswap((uint32_t)Sp);
+            if (((best - 1) >> 6) != h) Sm = Smo;
+            if (((best + 1) >> 6) != h) Sp = Spo;
+        }
+        if (h == 0 && own) {
+            const int mC = Mv[pix];
+            const int base = NDIR * (mC - e.P2);  // S = min(base + S', MAX_COST)
+            const int bm = max(best - 1, 0), bp = min(best + 1, D - 1);
+            const int cb0 = min(bm & ~1, D - 4);
+            const bool need = Sm >= clampS || Sp >= clampS;
+            const uint2 cw = *(const uint2*)(C + (need ? pix * D + cb0 : 0));
+            auto cword = [&](int d) -> int {
+                const int i = d - cb0;
+                const uint32_t wv = (i & 2) ? cw.y : cw.x;
+                return (int)((i & 1) ? (wv >> 16) : (wv & 0xffffu));
+            };
+            auto exact = [&](int Spp, int cv) -> int {
+                const int c1 = Spp >= clampS ? cv - mC : 0;
+                return min(base + Spp + NDIR * (c1 - min(c1, 2 * e.P2)), kMaxCost);
+            };
+            const int minS = min(base + mins, kMaxCost);
+            const int Smx = exact(Sm, cword(bm)), Spx = exact(Sp, cword(bp));
+            int bst = best;
+            if (minS >= kMaxCost) bst = -1;  // no strict minimum below MAX_COST
+            const int den = max(Smx + Spx - 2 * minS, 1);
+            const int frac = ((Smx - Spx) * kDispScale + den) / (den * 2);
+            const int d16 = bst * kDispScale + (frac & -(int)(0 < bst && bst < D - 1));
+            orow[x + minX1] = (int16_t)(d16 + minD * kDispScale);
+            const int x2 = x + minX1 - bst - minD;
+            if (minS < kMaxCost && x2 >= 0 && x2 < W)
+                atomicMin(krow + x2, ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    // left-right check (OpenCV 3.4 final loop) -- reads the finished row
+    for (int x = minX1 + threadIdx.x; x < e.maxX1; x += kBsWtaThreads) {
+        const int v = orow[x];
+        if (v == INV) continue;
+        const int dlo = v >> kDispShift, dhi = (v + kDispScale - 1) >> kDispShift;
+        const int xl = x - dlo, xh = x - dhi;
+        auto d2at = [&](int xx) -> int {
+            const uint32_t kk = __hip_atomic_load(krow + xx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (kk == 0xffffffffu) return INV;
+            const int xc = 0xffff - (int)(kk & 0xffffu);
+            return xc + minX1 - xx;
+        };
+        if (0 <= xl && xl < W && 0 <= xh && xh < W) {
+            const int a = d2at(xl), b = d2at(xh);
+            if (a >= minD && abs(a - dlo) > e.disp12 && b >= minD && abs(b - dhi) > e.disp12)
+                orow[x] = (int16_t)INV;
+        }
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+bool bsgm_eligible(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H)
+{
+    const long bs = 2L * e.SW2 + 1;
+    const bool no_wrap = (long)e.P2 + bs * bs * (2L * e.ftzero + 63) + e.P2 <= 32767;
+    return ctx->bitslice && e.fullDP && e.D == 128 && e.P1 == 2 && e.P2 == 5 && e.uniq == 0 && no_wrap &&
+           e.W1 > 0 && (size_t)n * H * e.W1 * 16 < ((size_t)1 << 31);
+}
+
+size_t bsgm_plane_bytes(int n, int H, int W1) { return (size_t)n * H * W1 * 64; }
+
+template <int NG>
+static int launch_bs_strips(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const uint32_t* Bv, uint32_t* Av,
+                            size_t aplane, uint32_t* dummy)
+{
+    using Cfg = BsStripCfg<NG>;
+    constexpr int npass = 2;
+    const int nstrips = (e.W1 + H - 1 + Cfg::kSW - 1) / Cfg::kSW;
+    const size_t bytes = (size_t)npass * n * nstrips * H * kBsGran * 8;
+    int rc;
+    if (ctx->bs_bnd.bytes < bytes) {
+        if ((rc = ensure(ctx, ctx->bs_bnd, bytes, "bit-sliced strip boundary granules"))) return rc;
+        // tag 0 (fresh memory) is never a launch epoch
+        if ((rc = check_hip(ctx, hipMemsetAsync(ctx->bs_bnd.ptr, 0, ctx->bs_bnd.bytes, ctx->stream),
+                            "bit-sliced boundary reset")))
+            return rc;
+    }
+    if (!ctx->status.ptr) {
+        if ((rc = ensure(ctx, ctx->status, 16, "device status words"))) return rc;
+        if ((rc = check_hip(ctx, hipMemsetAsync(ctx->status.ptr, 0, 16, ctx->stream), "status reset"))) return rc;
+        ctx->tri_tickets = 0;
+    }
+    // one epoch counter with the packed strip kernel: 32-bit tags here never repeat
+    if ((++ctx->tri_epoch & 0xffffu) == 0) ++ctx->tri_epoch;
+    const unsigned epoch = ctx->tri_epoch;
+    const dim3 grid(nstrips * npass * n);
+    const bool tickets = ctx->strip_tickets != 0;
+    // MVSV_BS_STATS: per-strip spans and hand-off spin time on stderr;
+    // MVSV_BS_NOWAIT: timing probe without the hand-off waits (maps wrong)
+    unsigned long long* stats = nullptr;
+    if (std::getenv("MVSV_BS_STATS")) {
+        (void)hipMalloc(&stats, (size_t)grid.x * 64);
+        (void)hipMemset(stats, 0, (size_t)grid.x * 64);
+    }
+    const bool nowait = std::getenv("MVSV_BS_NOWAIT") != nullptr;
+    if (Cfg::kBytes > 65536 &&
+        (rc = check_hip(ctx, hipFuncSetAttribute((const void*)bsgm_strip_kernel<NG, 2, 5>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::kBytes),
+                        "bit-sliced strip LDS attribute")))
+        return rc;
+    hipLaunchKernelGGL((bsgm_strip_kernel<NG, 2, 5>), grid, dim3(Cfg::kThreads), Cfg::kBytes, ctx->stream, Bv, Av,
+                       aplane, dummy, H, e.W1, npass, (unsigned long long*)ctx->bs_bnd.ptr, epoch, n,
+                       (int*)ctx->status.ptr, ctx->spin_limit, ctx->report_target,
+                       tickets ? (long long)ctx->tri_tickets : -1ll, stats, nowait ? 1 : 0);
+    rc = check_hip(ctx, hipGetLastError(), "bit-sliced strip kernel");
+    if (rc == MVSV_OK && tickets) ctx->tri_tickets += grid.x;
+    if (stats) {
+        (void)hipStreamSynchronize(ctx->stream);
+        std::vector<unsigned long long> hv((size_t)grid.x * 8);
+        (void)hipMemcpy(hv.data(), stats, hv.size() * 8, hipMemcpyDeviceToHost);
+        (void)hipFree(stats);
+        unsigned long long t0 = ~0ull, t1 = 0, spin = 0, busy = 0, steps = 0;
+        for (size_t b = 0; b < grid.x; b++) {
+            const unsigned long long* q = &hv[b * 8];
+            if (!q[1]) continue;
+            t0 = std::min(t0, q[0]);
+            t1 = std::max(t1, q[1]);
+            spin += q[2];
+            busy += q[1] - q[0];
+            steps += q[4];
+        }
+        std::fprintf(stderr, "[bs] NG %d strips %d blocks %u span %llu ticks, block-ticks %llu, spin %.1f%%, ticks/step %.1f\n",
+                     NG, nstrips, grid.x, t1 - t0, busy, 100.0 * spin / std::max(busy, 1ull),
+                     (double)busy / std::max(steps, 1ull));
+    }
+    return rc;
+}
+
+int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv, const uint32_t* Bv,
+               const uint16_t* Mv, int16_t* raw)
+{
+    int rc;
+    const size_t aplane = (size_t)n * H * e.W1 * 16;  // words per strip-pass plane
+    const size_t dplane = (size_t)n * H * e.W1 * 12;  // words per line plane
+    // + 512 words: the strip kernel's dummy store slots (cells outside the image)
+    if ((rc = ensure(ctx, ctx->agg, (2 * aplane + 2 * dplane + 512) * 4, "bit-sliced delta planes"))) return rc;
+    if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
+    uint32_t* Av = (uint32_t*)ctx->agg.ptr;
+    uint32_t* Dv = Av + 2 * aplane;
+    hipStream_t s = ctx->stream;
+    if (!ctx->aux) {
+        if ((rc = check_hip(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking), "aux stream")) ||
+            (rc = check_hip(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming), "event")) ||
+            (rc = check_hip(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming), "event")))
+            return rc;
+    }
+    {
+        StageTimer tm(ctx, kStagePath);
+        if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_fork, s), "fork")) ||
+            (rc = check_hip(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0), "fork wait")))
+            return rc;
+        // the row directions beside the strips (different units of work: the
+        // strip chain leaves SIMDs idle while it fills and drains); bs_serial:
+        // after them on the context stream (A/B, isolated stage times)
+        hipStream_t ls = ctx->bs_serial ? s : ctx->aux;
+        auto lines = [&]() -> int {
+            StageTimer tl(ctx, kStageLines, ls);
+            hipLaunchKernelGGL((bsgm_lines_kernel<2, 5>), dim3((H + 31) / 32, n, 2), dim3(64), 0, ls, Bv, Dv,
+                               dplane, H, e.W1, std::getenv("MVSV_BS_PROBE") ? 1 : 0);
+            return check_hip(ctx, hipGetLastError(), "bit-sliced line kernel");
+        };
+        if (!ctx->bs_serial && (rc = lines())) return rc;
+        {
+            StageTimer ts(ctx, kStageStrips);
+            const int ng = ctx->bs_groups;
+            uint32_t* dummy = Dv + 2 * dplane;
+            rc = ng == 1 ? launch_bs_strips<1>(ctx, n, H, e, Bv, Av, aplane, dummy)
+                 : ng == 4 ? launch_bs_strips<4>(ctx, n, H, e, Bv, Av, aplane, dummy)
+                           : launch_bs_strips<2>(ctx, n, H, e, Bv, Av, aplane, dummy);
+            if (rc) return rc;
+        }
+        if (ctx->bs_serial && (rc = lines())) return rc;
+        if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_join, ctx->aux), "join")) ||
+            (rc = check_hip(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0), "join wait")))
+            return rc;
+    }
+    StageTimer tm(ctx, kStageFinal);
+    hipLaunchKernelGGL(bsgm_wta_kernel, dim3(H, n), dim3(kBsWtaThreads), 0, s, Bv, Av, aplane, Dv, dplane, Cv, Mv, H,
+                       W, e, raw, (uint32_t*)ctx->keys.ptr);
+    return check_hip(ctx, hipGetLastError(), "bit-sliced WTA kernel");
+}
+
+}  // namespace mvsv

@@ -285,6 +285,12 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
     }
     if (const char* v = std::getenv("MVSV_STRIP_ORDER")) c->strip_tickets = std::strcmp(v, "blockidx") != 0;
     if (const char* v = std::getenv("MVSV_LINES_AUX")) c->lines_aux = std::max(-1, std::min(2, std::atoi(v)));
+    if (const char* v = std::getenv("MVSV_BITSLICE")) c->bitslice = std::atoi(v) != 0;
+    if (const char* v = std::getenv("MVSV_BS_SERIAL")) c->bs_serial = std::atoi(v) != 0;
+    if (const char* v = std::getenv("MVSV_BS_GROUPS")) {
+        const int g = std::atoi(v);
+        c->bs_groups = (g == 1 || g == 4) ? g : 2;
+    }
     *out = c;
     return MVSV_OK;
 }
@@ -302,7 +308,7 @@ int mvsv_trim(mvsv_ctx* ctx)
     DeviceGuard dev_guard(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     DevBuf* all[] = {&ctx->pre, &ctx->cost, &ctx->cres, &ctx->agg, &ctx->raw, &ctx->uf_parent, &ctx->uf_size, &ctx->uf_lroot, &ctx->uf_list,
-                     &ctx->uf_tile, &ctx->tri_bnd, &ctx->status,
+                     &ctx->uf_tile, &ctx->tri_bnd, &ctx->bs_bnd, &ctx->status,
                      &ctx->dummy, &ctx->keys,
                      &ctx->bm_lf, &ctx->bm_rf, &ctx->bm_cost, &ctx->bm_sad, &ctx->h_left, &ctx->h_right,
                      &ctx->h_out};
@@ -435,6 +441,10 @@ int mvsv_set_option(mvsv_ctx* ctx, int option, long long value)
     case MVSV_OPT_COST_RESIDUAL:
         if (value < 0 || value > 1) return set_error(ctx, MVSV_E_INVALID_ARG, "cost residual must be 0 or 1");
         ctx->cost_res = (int)value;
+        return MVSV_OK;
+    case MVSV_OPT_BITSLICE:
+        if (value < 0 || value > 1) return set_error(ctx, MVSV_E_INVALID_ARG, "bitslice must be 0 or 1");
+        ctx->bitslice = (int)value;
         return MVSV_OK;
     default:
         return set_error(ctx, MVSV_E_INVALID_ARG, "unknown option");

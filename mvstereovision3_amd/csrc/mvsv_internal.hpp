@@ -89,7 +89,7 @@ struct mvsv_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // SGBM
-    mvsv::DevBuf pre, cost, cres, agg, raw, uf_parent, uf_size, uf_tile, uf_lroot, uf_list, dummy, keys, tri_bnd, status;
+    mvsv::DevBuf pre, cost, cres, agg, raw, uf_parent, uf_size, uf_tile, uf_lroot, uf_list, dummy, keys, tri_bnd, bs_bnd, status;
     bool uf_list_dirty = false;  // a speckle run launched its first stage but not its last
     // launch number of the last sheared-strip launch: its low 16 bits tag the
     // boundary granules (tri_bnd is re-zeroed whenever they wrap), all 32 bits
@@ -125,6 +125,9 @@ struct mvsv_ctx {
     int strip_waves = 0;  // compute waves per strip (0 = by launch size; 4 or the wide count forces)
     int cost_res = 1;     // direction passes read the cost residual plane where exact (MVSV_OPT_COST_RESIDUAL)
     int lines_aux = -1;  // L->R line kernel beside the strip kernel: -1 = small launches only, 0 / 1 / 2 force
+    int bitslice = 1;    // bit-sliced MODE_HH paths where they apply (MVSV_OPT_BITSLICE, env MVSV_BITSLICE)
+    int bs_groups = 2;   // column groups (3 direction waves each) per bit-sliced strip: 1, 2, 4 (MVSV_BS_GROUPS)
+    int bs_serial = 0;   // 1: bit-sliced line kernel after the strips on one stream (MVSV_BS_SERIAL, A/B)
     int bm2 = 1;     // StereoBM: disparities-on-lanes match kernel where blockSize <= 21, D <= 128
     int bm_ty = 0;   // its tile height (0 = chosen per launch); MVSV_BM_TY for A/B runs
     int cus = 256;   // compute units of the device (launch-shape choices)
@@ -190,6 +193,13 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
 // poison != nullptr: when *poison == epoch (the launch `epoch` gave up a strip
 // wait) every output pixel is `invalid` instead of the median -- no map computed
 // from stale hand-off data leaves the pipeline.
+// Bit-sliced MODE_HH path aggregation + WTA (mvsv_bsgm.hip).  bsgm_eligible:
+// the parameters admit it; the cost kernel then writes the C' planes Bv
+// (bsgm_plane_bytes) and bsgm_paths computes raw disparities from them.
+bool bsgm_eligible(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H);
+size_t bsgm_plane_bytes(int n, int H, int W1);
+int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv, const uint32_t* Bv,
+               const uint16_t* Mv, int16_t* raw);
 int median3x3_device(mvsv_ctx* ctx, int n, const int16_t* src, size_t ss, size_t sfs,
                      int16_t* dst, size_t ds, size_t dfs, int W, int H,
                      const int* poison = nullptr, unsigned epoch = 0, int invalid = 0);

@@ -26,6 +26,7 @@
 
 #include "mvsv_cost_layout.hpp"
 #include "mvsv_device.hpp"
+#include "mvsv_bitslice.hpp"
 #include "mvsv_internal.hpp"
 
 #ifndef MVSV_COST2_FETCH_DEPTH
@@ -391,12 +392,49 @@ __device__ __forceinline__ uint32_t bt_cost2(uint4 u4, uint2 u2, uint4 v4, uint2
     return add2_nc(ca, __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, cb) >> two));
 }
 
+// 32 x 32 bit transpose inside each 32-lane half of the wave: afterwards lane q
+// (of its half) holds bit q of every lane p's input word, as bit p.  Five
+// delta-swap stages, lane distance s = 16 .. 1 against word-bit distance s
+// (the host mirror in tests/cpp/bitslice_check.cpp checks the same stages):
+// 16- and 8-bit fields move as bytes (v_permlane16_swap / DPP row_ror:8 + one
+// v_perm_b32), 4-, 2- and 1-bit fields by rotating the partner's word and one
+// v_bfi_b32 with the lane's keep mask.
+__device__ __forceinline__ uint32_t bs_rotmix(uint32_t own, uint32_t pt, bool upper, int s, uint32_t M)
+{
+    const uint32_t sh = bs::fshr(pt, pt, upper ? s : 32 - s);
+    const uint32_t K = upper ? ~M : M;
+    return (K & own) | (~K & sh);
+}
+__device__ __forceinline__ uint32_t bs_transpose32(uint32_t x, int lane)
+{
+    {
+        // rows (0, 1) and (2, 3) of the wave swap halves: r[0] keeps even rows
+        // and receives the odd rows' words, r[1] the reverse
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        x = __builtin_amdgcn_perm(r[1], r[0], (lane & 16) ? 0x07060302u : 0x05040100u);
+    }
+    {
+        const uint32_t pt = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xf, 0xf, true);  // row_ror:8 = lane ^ 8
+        x = __builtin_amdgcn_perm(pt, x, (lane & 8) ? 0x03070105u : 0x06020400u);
+    }
+    {
+        // lane ^ 4: row_shl:4 into banks 0 and 2, row_shr:4 into banks 1 and 3
+        int pt = __builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xf, 0x5, false);
+        pt = __builtin_amdgcn_update_dpp(pt, (int)x, 0x114, 0xf, 0xa, false);
+        x = bs_rotmix(x, (uint32_t)pt, (lane & 4) != 0, 4, 0x0F0F0F0Fu);
+    }
+    x = bs_rotmix(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xf, 0xf, true), (lane & 2) != 0, 2, 0x33333333u);
+    x = bs_rotmix(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xf, 0xf, true), (lane & 1) != 0, 1, 0x55555555u);
+    return x;
+}
+
 template <int NR, int STG, int PPC>
 __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4))) void sgbm_cost2_kernel(const uint64_t* __restrict__ pre,
                                                                    int W, int H, SgbmEff e, int TY,
                                                                    int16_t* __restrict__ C,
                                                                    uint8_t* __restrict__ Rv,
-                                                                   uint16_t* __restrict__ Mv)
+                                                                   uint16_t* __restrict__ Mv,
+                                                                   uint32_t* __restrict__ Bv)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int SH2 = NR / 2;
@@ -632,7 +670,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                 // minima per lane, then one transposing step (even lanes keep
                 // reducing columns (0, 1), odd lanes (2, 3)) and five
                 // parity-preserving butterfly steps on a single dword.
-                if (Rv && emit) {
+                if ((Rv || (PPC == 64 && Bv)) && emit) {
                     const uint32_t Plo01 = __builtin_amdgcn_perm(ov[1], ov[0], 0x05040100u);
                     const uint32_t Phi01 = __builtin_amdgcn_perm(ov[1], ov[0], 0x07060302u);
                     const uint32_t Plo23 = __builtin_amdgcn_perm(ov[3], ov[2], 0x05040100u);
@@ -661,6 +699,28 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                         const uint32_t ab = p < 2 ? A : B;
                         Mv[(size_t)(orow - (uint32_t*)C) / PP + p] = (uint16_t)(p & 1 ? ab >> 16 : ab);
                     }
+                    if constexpr (PPC == 64) {
+                        if (Bv) {
+                            // bit-sliced C' = min(C - m, 2 P2) (round 5, mvsv_bitslice.hpp):
+                            // nibble bytes as below but without the + P2 bias, columns in
+                            // byte order (0, 2, 1, 3), then a 32 x 32 bit transpose inside
+                            // each 32-lane half: lane l ends with word (h, e, b) of column
+                            // c, bit p = bit b of C'(c, 64 h + 2 p + e) -- one dword store
+                            // per lane, the wave's four pixels as one 256-byte record run
+                            // (C' <= 2 P2 <= 10: the subtractions never borrow, m <= C)
+                            const uint32_t p2x4 = add2_nc(p2x2, p2x2);
+                            const uint32_t r01 = pk_min_u16(sub2_nb(Plo01, A), p2x4) |
+                                                 (pk_min_u16(sub2_nb(Phi01, A), p2x4) << 4);
+                            const uint32_t r23 = pk_min_u16(sub2_nb(Plo23, B), p2x4) |
+                                                 (pk_min_u16(sub2_nb(Phi23, B), p2x4) << 4);
+                            const uint32_t tw = bs_transpose32(r01 | (r23 << 8), p);
+                            const int q = p & 31, k = q >> 3;
+                            const int c = ((k & 1) << 1) | (k >> 1);
+                            uint32_t* brow = Bv + (size_t)(orow - (uint32_t*)C) / PP * 16;
+                            if (full || c < nout) brow[c * 16 + (p >> 5) * 8 + (q & 7)] = tw;
+                        }
+                    }
+                    if (Rv) {
                     // R = min(C - m, 2 P2) + P2 = min(C - (m - P2), 3 P2) on the
                     // column pairs; one word holds columns 0 and 1's residual
                     // bytes R[2p] | R[2p+1] << 4 in bits 0-7 and 16-23
@@ -677,6 +737,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
                     for (int i = 0; i < kCost2Run; i++)
                         if (full || i < nout) rrow[i * PP] = (uint8_t)rw[i];
+                    }
                 }
             }
         }
@@ -3103,7 +3164,7 @@ int launch_paths_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
 
 }  // namespace
 
-using Cost2Kern = void (*)(const uint64_t*, int, int, SgbmEff, int, int16_t*, uint8_t*, uint16_t*);
+using Cost2Kern = void (*)(const uint64_t*, int, int, SgbmEff, int, int16_t*, uint8_t*, uint16_t*, uint32_t*);
 template <int STG, int PPC>
 static Cost2Kern cost2_pick_nr(int nr)
 {
@@ -3132,7 +3193,8 @@ static Cost2Kern cost2_pick(int nr, int stg, int ppc)
 // is written by the register-ring kernel only: the LDS-ring fallback sets it
 // to nullptr, and the direction passes then read C.
 static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int TY,
-                       const uint64_t* pre, int16_t* Cv, uint8_t** Rv, uint16_t* Mv, bool* pinned_hh)
+                       const uint64_t* pre, int16_t* Cv, uint8_t** Rv, uint16_t* Mv, bool* pinned_hh,
+                       uint32_t** Bv)
 {
     *pinned_hh = false;
     hipStream_t s = ctx->stream;
@@ -3148,6 +3210,7 @@ static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int
             // numDisparities 128 / 256: the pair count is a compile-time
             // constant (unrolled pixel-cost loop, immediate LDS offsets)
             const int ppc = !ctx->cost_fixed_pp ? 0 : l2.PP == 64 ? 64 : (l2.PP == 128 ? 128 : 0);
+            if (ppc != 64) *Bv = nullptr;  // the bit-sliced plane: D = 128 kernels only
             kern = cost2_pick(2 * e.SH2 + 1, two ? 2 : 1, ppc);
             if (l2.bytes > 65536 &&
                 (rc = check_hip(ctx, hipFuncSetAttribute((const void*)kern,
@@ -3158,13 +3221,14 @@ static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int
             {
                 StageTimer tm(ctx, kStageCost);
                 hipLaunchKernelGGL(kern, grid2, dim3(kCost2Threads), l2.bytes, s, pre, W, H, e, TY,
-                                   Cv, *Rv, Mv);
+                                   Cv, *Bv ? nullptr : *Rv, Mv, *Bv);
             }
             *pinned_hh = e.fullDP != 0;  // MODE_HH fix-up rows/column written by the kernel
             return check_hip(ctx, hipGetLastError(), "sgbm cost kernel");
         }
     }
     *Rv = nullptr;
+    *Bv = nullptr;
     CostLayout lay = cost_layout(e.D, e.SW2, e.SH2, TY);
     if (lay.nLmax + lay.nRmax + 1 > 256 * kStageRegs)
         return set_error(ctx, MVSV_E_INVALID_ARG, "numDisparities too large for the GPU cost kernel");
@@ -3200,6 +3264,12 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     const size_t vol = (size_t)e.W1 * H * e.D;
     if ((rc = ensure(ctx, ctx->pre, (size_t)n * 2 * plane * 8, "sgbm BT interval planes"))) return rc;
     if ((rc = ensure(ctx, ctx->cost, (size_t)n * vol * 2, "sgbm cost volume"))) return rc;
+    // bit-sliced MODE_HH paths (round 5, mvsv_bsgm.hip): the cost kernel writes
+    // the C' bit planes instead of the residual nibbles; the planes of the
+    // direction passes are sized by bsgm_paths
+    const bool bs = bsgm_eligible(ctx, e, n, H) && ctx->path16 && ctx->tri && ctx->cost2 && ctx->cost_fixed_pp &&
+                    e.SH2 <= 7 && e.SW2 == e.SH2;
+    uint32_t* Bv = nullptr;
     // accumulator planes: one per concurrently written direction group
     const int sched = path_schedule(ctx, e, H, n);
     const int nplanes = sched == 2 ? (e.fullDP ? 7 : 4) : sched == 1 ? (e.fullDP ? 3 : 2) : 1;
@@ -3207,16 +3277,22 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     // pass + lines; bytes / u16 otherwise (side by side: one delta <= P2 each)
     const bool nib = (sched == 2 && e.P2 <= 15) || (sched == 1 && nplanes > 1 && acc_is_nib(e));
     const bool u8 = acc_is_u8(e);
-    if ((rc = ensure(ctx, ctx->agg, nib ? (size_t)nplanes * n * vol / 2
-                                        : (size_t)nplanes * n * vol * (u8 ? 1 : 2),
-                     "sgbm path-delta accumulator")))
+    if (!bs && (rc = ensure(ctx, ctx->agg, nib ? (size_t)nplanes * n * vol / 2
+                                               : (size_t)nplanes * n * vol * (u8 ? 1 : 2),
+                            "sgbm path-delta accumulator")))
         return rc;
     if ((rc = ensure(ctx, ctx->raw, (size_t)n * plane * 2, "sgbm raw disparity"))) return rc;
     // residual plane for the direction passes (0.5 byte per cost instead of 2)
     // + the per-pixel cost minimum (u16 per cost column) behind it
     uint8_t* Rv = nullptr;
     uint16_t* Mv = nullptr;
-    if (use_residual(ctx, e, sched)) {
+    if (bs) {
+        const size_t bbytes = (bsgm_plane_bytes(n, H, e.W1) + 255) & ~(size_t)255;
+        if ((rc = ensure(ctx, ctx->cres, bbytes + (size_t)n * e.W1 * H * 2, "sgbm bit-sliced cost planes")))
+            return rc;
+        Bv = (uint32_t*)ctx->cres.ptr;
+        Mv = (uint16_t*)((uint8_t*)ctx->cres.ptr + bbytes);
+    } else if (use_residual(ctx, e, sched)) {
         const size_t rbytes = (n * vol / 2 + 255) & ~(size_t)255;
         if ((rc = ensure(ctx, ctx->cres, rbytes + (size_t)n * e.W1 * H * 2, "sgbm cost residual plane"))) return rc;
         Rv = (uint8_t*)ctx->cres.ptr;
@@ -3263,7 +3339,16 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
         }
     }
     bool pinned_hh = false;
-    if ((rc = launch_cost(ctx, n, W, H, e, TY, pre, Cv, &Rv, Mv, &pinned_hh))) return rc;
+    if ((rc = launch_cost(ctx, n, W, H, e, TY, pre, Cv, &Rv, Mv, &pinned_hh, &Bv))) return rc;
+    if (bs && !Bv) {
+        // the cost kernel could not write the planes (a launch shape without
+        // the D = 128 register-ring kernel): the packed kernels on C
+        if ((rc = ensure(ctx, ctx->agg, nib ? (size_t)nplanes * n * vol / 2
+                                            : (size_t)nplanes * n * vol * (u8 ? 1 : 2),
+                         "sgbm path-delta accumulator")))
+            return rc;
+        Sv = ctx->agg.ptr;
+    }
 
     const int ybot = std::max(H - e.SH2, 1);     // first row that is never recomputed
     const int ylast = std::max(H - e.SH2 - 1, 0);  // last recomputed row
@@ -3286,7 +3371,9 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
 
     const int np = (e.D + 127) / 128;
     const bool wide = ctx->path16 && (e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256);
-    if (wide) {
+    if (Bv) {
+        rc = bsgm_paths(ctx, n, H, W, e, Cv, Bv, Mv, raw);
+    } else if (wide) {
         switch (e.D) {
         case 32: rc = launch_paths16_acc<1>(ctx, n, H, W, e, Cv, Rv, Mv, Sv, raw); break;
         case 64: rc = launch_paths16_acc<2>(ctx, n, H, W, e, Cv, Rv, Mv, Sv, raw); break;

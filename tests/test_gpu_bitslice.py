@@ -1,0 +1,82 @@
+"""Bit-sliced MODE_HH path aggregation (round 5, mvsv_bsgm.hip): where it applies
+(MODE_HH, numDisparities 128, P1 2 / P2 5 -- configs/sgbm.yml's effective penalties
+--, uniquenessRatio 0, no int16 wrap) the six strip directions, the two row
+directions and the WTA run on bit planes.  Every case runs with the bit-sliced
+path (the default) and forced off (MVSV_OPT_BITSLICE = 0, the packed int16
+kernels), and both must be bit-exact against the oracle.
+Reference: Disparity::sgbm (src/disparity.cpp:6-10) -> cv::StereoSGBM::compute;
+mode from loadSGBMParameters (src/disparity.cpp:92-95)."""
+import numpy as np
+import pytest
+
+from tests.test_gpu_parity import rand_pair, report, sgbm_both
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # (H, W, blockSize, P1, P2, minD, disp12)
+    (40, 200, 13, 2, 5, 1, 0),      # configs/sgbm.yml shape (P1 / P2 given)
+    (53, 231, 13, 0, 0, 1, 0),      # sgbm.yml as loaded: P1 = P2 = 0 -> 2 / 5
+    (31, 190, 3, 2, 5, 0, 2),       # small window
+    (64, 300, 15, 0, 0, -3, 1),     # largest register-ring window, negative minDisparity
+    (17, 140, 9, 2, 5, 4, -1),      # short image: few strips, chain of one
+    (120, 420, 11, 0, 0, 1, 3),     # several strips per chain, both passes
+    (9, 135, 5, 0, 0, 0, 0),        # fewer rows than the window (pinned rows only)
+    (90, 129 + 127, 7, 2, 5, 0, 0), # W1 = 128: a single strip column group edge
+]
+
+
+@pytest.mark.parametrize("bits", [1, 0])
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_bitslice_hh_forced(gpu, mvsv, oracle, case, bits):
+    from mvstereovision3_amd import _lib
+    H, W, bs, P1, P2, minD, d12 = CASES[case]
+    rng = np.random.default_rng(5100 + 7 * case)
+    kind = case % 3
+    L, R = rand_pair(rng, H, W, int(rng.integers(0, 60)), kind)
+    kw = dict(minDisparity=minD, numDisparities=128, blockSize=bs, P1=P1, P2=P2, disp12MaxDiff=d12,
+              uniquenessRatio=0, speckleWindowSize=int(rng.choice([0, 20])), speckleRange=2, mode=1)
+    variant = int(rng.integers(0, 4))
+    try:
+        _lib.set_option(_lib.OPT_BITSLICE, bits)
+        got, want = sgbm_both(mvsv, oracle, L, R, variant=variant, **kw)
+    finally:
+        _lib.set_option(_lib.OPT_BITSLICE, 1)
+    assert np.array_equal(got, want), f"bitslice={bits} variant={variant} {kw}: " + report(got, want)
+
+
+@pytest.mark.parametrize("groups", ["1", "2", "4"])
+def test_bitslice_strip_groups(gpu, mvsv, oracle, groups, monkeypatch):
+    """Every strip width (column groups per strip) on a 3-frame device batch."""
+    from mvstereovision3_amd import _lib
+    torch = gpu
+    monkeypatch.setenv("MVSV_BS_GROUPS", groups)
+    ctx = _lib.Context(0)  # a fresh context reads the environment
+    rng = np.random.default_rng(5200 + int(groups))
+    H, W, D = 72, 330, 128
+    pairs = [rand_pair(rng, H, W, int(rng.integers(0, 50)), k % 3) for k in range(3)]
+    m = mvsv.StereoSGBM.create(minDisparity=1, numDisparities=D, blockSize=13, P1=0, P2=0, disp12MaxDiff=0,
+                               uniquenessRatio=0, mode=1)
+    dev = torch.device("cuda", 0)
+    Lb = torch.from_numpy(np.stack([q[0] for q in pairs])).to(dev)
+    Rb = torch.from_numpy(np.stack([q[1] for q in pairs])).to(dev)
+    out = torch.empty((3, H, W), dtype=torch.int16, device=dev)
+    try:
+        with _lib.use_context(ctx):
+            m.compute(Lb, Rb, out)
+            _lib.synchronize(0)
+        got = out.cpu().numpy()
+    finally:
+        ctx.close()
+    p = dict(min_disparity=1, num_disparities=D, block_size=13, p1=0, p2=0, disp12_max_diff=0,
+             pre_filter_cap=0, uniqueness_ratio=0, speckle_window_size=0, speckle_range=0, mode=1)
+    for i, (L, R) in enumerate(pairs):
+        want = oracle.sgbm(L, R, p)
+        assert np.array_equal(got[i], want), f"groups={groups} frame {i}: " + report(got[i], want)
+
+
+def test_bitslice_option_range(gpu):
+    from mvstereovision3_amd import _lib
+    for bad in (-1, 2):
+        with pytest.raises(_lib.MvsvError):
+            _lib.set_option(_lib.OPT_BITSLICE, bad)
