@@ -119,7 +119,7 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True, res=False):
+def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True, res=False, bits=False):
     """Implementation HBM bytes of one step per stage ("Kernels").
 
     acc = bytes per (pixel, disparity) of a path-delta accumulator plane (0.5 for
@@ -130,11 +130,30 @@ def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True, res=False):
     line kernel reads its cost input and writes a plane, the final kernel reads C
     and every plane.  res = the direction passes read the nibble cost residual
     plane (0.5 B per cost, written by the cost kernel beside C) instead of C.
+    bits = the bit-sliced MODE_HH pipeline (mvsv_bsgm.hip): the
+    cost kernel writes C (read back only at best -+ 1) and the 4-bit C' planes,
+    the strip passes read C' and write a 4-bit plane each, the two line
+    directions read C' and write 3-bit planes, the WTA reads C', every plane and
+    the gathered costs.
     """
     cells = W1 * H * D
     px = W * H
     npass = 2 if ndir == 8 else 1
     cin = 0.5 if res else 2
+    if bits:
+        strip_b = F * cells * 2 * (0.5 + 0.5)
+        lines_b = F * cells * 2 * (0.5 + 0.375)
+        return {
+            "prefilter": F * (2 * px + 2 * 8 * px),
+            "cost_volume": F * (2 * 8 * px + 2.5 * cells + 2 * W1 * H),
+            "path_aggregation": strip_b + lines_b,
+            "path_strips": strip_b,
+            "path_lines": lines_b,
+            # C', two strip planes, two line planes; minimum, gathered costs,
+            # raw map and right-view keys per pixel
+            "final_wta_lr": F * (cells * (0.5 + 2 * 0.5 + 2 * 0.375) + W1 * H * (2 + 8) + 6 * px),
+            "post_filters": F * 4 * px,
+        }.get(stage, 0)
     if strips:
         planes = npass + 1
         strip_b = F * cells * npass * (cin + acc)
@@ -438,6 +457,11 @@ def main(argv=None):
     ftzero = max(params["pre_filter_cap"], 15) | 1
     residual = (os.environ.get("MVSV_COST_RESIDUAL", "1") != "0" and D in (32, 64, 128) and 3 * P2 <= 15
                 and 2 * P2 + bs * bs * (2 * ftzero + 63) <= 32767)
+    # the bit-sliced MODE_HH pipeline (MVSV_OPT_BITSLICE; frame batches on the
+    # strip schedule): sgbm.yml's P1 2 / P2 5, D 128, uniquenessRatio 0
+    uq = params["uniqueness_ratio"]
+    bitslice = (os.environ.get("MVSV_BITSLICE", "1") != "0" and ndir == 8 and D == 128 and P1 == 2 and P2 == 5
+                and uq == 0 and 2 * P2 + bs * bs * (2 * ftzero + 63) <= 32767 and F >= 2)
 
     from mvstereovision3_amd.batch import FrameBatch, InflightBatches, frame_seeds
     host = [mvsv.synth_pair(sd, W, H, minD, D) for sd in frame_seeds(rank, world, F, SEED0)]
@@ -532,7 +556,7 @@ def main(argv=None):
         comp = 4 * W * H * (1 + D)
         alg_bytes_per_launch = comp * F / launches
         achieved = alg_bytes_per_launch / avg_launch_s / 1e9
-        impl_bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir, acc, strips, residual) / launches
+        impl_bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir, acc, strips, residual, bitslice) / launches
         workload = f"sgbm_{W}x{H}_d{D}_{ndir}path_batch{F}"
         sha = kernel_source_sha()
         pmc, traffic_note = _summary(PMC_FILE, workload, sha, "PMC")

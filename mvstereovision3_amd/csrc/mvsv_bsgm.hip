@@ -15,7 +15,7 @@
 //   bsgm_strip_kernel  the six vertical / diagonal directions of both passes on
 //                      sheared strips (the strip chain, tickets and boundary
 //                      hand-off of sgbm_tri_kernel), one wave per direction
-//   bsgm_lines_kernel  L->R and R->L along the rows
+//   bsgm_lines4_kernel L->R and R->L along the rows (a pixel on a lane quad)
 //   bsgm_wta_kernel    S'' = 8 C' + sum of deltas, argmin (smallest d), exact
 //                      S(best -+ 1) for the parabola, right-view keys, LR check
 //
@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -88,6 +89,44 @@ __device__ __forceinline__ void bs_dir_step(const uint32_t (&sE)[3], const uint3
     }
     bs::subclamp<P2>(vE, M[0], M[1], M[2], nE);
     bs::subclamp<P2>(vO, M[0], M[1], M[2], nO);
+}
+
+// The same step with a pixel on a lane quad, q = 2 h + e: the lane holds only
+// the parity-e words of half h, so a step is half the instructions per lane
+// (one delta, one add, one clamp) for twice the lanes -- the serial chains of a
+// pass run at half the latency per step.  Neighbours: d -+ 1 of an even word
+// is the partner word (lane q ^ 1) and, shifted in, the odd word of the lane
+// below (q - 1); of an odd word the partner and the even word of q + 1.  One
+// v_alignbit of (hi = quad lane q + 1, lo = q - 1) by 31 (even) / 1 (odd)
+// gives the shifted neighbour, the partner is lo (odd) or hi (even).
+// fill_hi / fill_lo: all-ones on q = 3 / q = 0 (d = 128 / -1: code 7 -> P2).
+template <int P1, int P2>
+__device__ __forceinline__ void bs_quad_step(const uint32_t (&s)[3], const uint32_t (&c)[4], uint32_t fill_hi,
+                                             uint32_t fill_lo, bool odd, uint32_t sh, uint32_t (&n)[3],
+                                             uint32_t (&d)[3])
+{
+    uint32_t nb[3], pt[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)s[k], 0xF9, 0xf, 0xf, true) | fill_hi;  // [1,2,3,3]
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)s[k], 0x90, 0xf, 0xf, true) | fill_lo;  // [0,0,1,2]
+        nb[k] = __builtin_amdgcn_alignbit(hi, lo, sh);
+        pt[k] = odd ? lo : hi;
+    }
+    bs::delta3<P1, P2>(s, nb, pt, d);
+    uint32_t v[4];
+    bs::add43(c, d, v);
+    uint32_t kk = ~v[3], M[3];
+#pragma unroll
+    for (int b = 2; b >= 0; b--) {
+        const uint32_t z = bs::lop3<bs::kAndNotAB>(v[b], kk, kk);
+        uint32_t any = z | xswap(z);
+        any |= (uint32_t)__builtin_amdgcn_mov_dpp((int)any, 0x4E, 0xf, 0xf, true);  // quad_perm [2,3,0,1]
+        const bool f = any != 0u;
+        if (b > 0) kk = f ? z : kk;
+        M[b] = f ? 0u : kOnes;
+    }
+    bs::subclamp<P2>(v, M[0], M[1], M[2], n);
 }
 
 // ---------------------------------------------------------------------------
@@ -399,86 +438,61 @@ __global__ __launch_bounds__(BsStripCfg<NG>::kThreads) void bsgm_strip_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Lines: L->R (blockIdx.z = 0) and R->L (1), 32 rows per wave, two lanes per
-// row; each writes its delta plane (3 bits).
+// Lines: L->R (blockIdx.z = 0) and R->L (1); each writes its delta plane (3 bits).
 // ---------------------------------------------------------------------------
-// One wave per block: 32 rows x 2 lanes.  The rows' C' records stream through
-// LDS in chunks of kBsChunk pixels -- each row's chunk is one contiguous
-// 512-byte run, loaded by whole-wave coalesced dwordx4 loads one chunk ahead
-// (registers -> padded LDS rows) -- because per-lane row loads (64 bytes from
-// each of 32 rows per step) measured 3x slower than the recurrence itself
-// (1.04 vs 0.33 ms for the 8-frame batch with every row reading one cached row).
-constexpr int kBsChunk = 8;
-constexpr int kBsLineRowB = kBsChunk * 64 + 16;  // LDS row stride (bytes): + 16 B against bank conflicts
-constexpr int kBsLineBufB = 32 * kBsLineRowB;
+// The lines on lane quads (bs_quad_step): 16 rows per wave, lane 4 r + q holds
+// words (h, e) = (q >> 1, q & 1) of row r -- 16 contiguous bytes of the C'
+// record and 12 of the delta record -- so the grid has twice the waves of a
+// lane-pair layout at two thirds of the instructions per step.  Each lane
+// loads its own 16 bytes kBsLPF steps ahead into registers (a load instruction
+// covers 16 rows x one 64-byte record): the pass is bound by the memory
+// parallelism of its few waves, not by their instructions.
+constexpr int kBsLPF = 16;
 
 template <int P1, int P2>
-__global__ __launch_bounds__(64) void bsgm_lines_kernel(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dl,
-                                                         size_t plane_words, int H, int W1, int probe)
+__global__ __launch_bounds__(64) void bsgm_lines4_kernel(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dl,
+                                                          size_t plane_words, int H, int W1)
 {
-    __shared__ __attribute__((aligned(16))) unsigned char lbuf[2 * kBsLineBufB];
     const int lane = threadIdx.x;
-    const int h = lane & 1, rr = lane >> 1;
-    const int y0 = (int)blockIdx.x * 32;
-    const int y = min(y0 + rr, H - 1);
+    const int q = lane & 3, rr = lane >> 2;
+    const int y = min((int)blockIdx.x * 16 + rr, H - 1);
     const int f = blockIdx.y;
     const bool rl = blockIdx.z != 0;
-    const uint32_t fill0 = h == 0 ? kOnes : 0u, fill1 = h == 1 ? kOnes : 0u;
-    uint32_t* drow = Dl + (rl ? plane_words : 0) + ((size_t)(f * H + y) * W1) * 12 + h * 6;
-    // loader: instruction i covers rows 2 i + (lane >> 5), 16-byte piece lane & 31
-    // of the chunk's 512 bytes (pixel sg >> 2, piece sg & 3)
-    const int sg = lane & 31;
-    const uint32_t* lrow[16];
+    const bool odd = (q & 1) != 0;
+    const uint32_t fill_hi = q == 3 ? kOnes : 0u, fill_lo = q == 0 ? kOnes : 0u, sh = odd ? 1u : 31u;
+    const size_t rowpix = (size_t)(f * H + y) * W1;
+    uint32_t* drow = Dl + (rl ? plane_words : 0) + rowpix * 12 + q * 3;
+    const uint32_t* crow = Bc + rowpix * 16 + q * 4;
+    // pixel of step t (clamped: loads past the row's end are issued, not used)
+    auto px = [&](int t) { return rl ? max(W1 - 1 - t, 0) : min(t, W1 - 1); };
+    uint4 cr[kBsLPF];
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-        const int yy = probe ? 0 : min(y0 + 2 * i + (lane >> 5), H - 1);
-        lrow[i] = Bc + ((size_t)((probe ? 0 : f) * H + yy) * W1) * 16 + (sg & 3) * 4;
-    }
-    uint4 stg[16];
-    const int nch = (W1 + kBsChunk - 1) / kBsChunk;
-    auto chunk_base = [&](int c) { return rl ? W1 - kBsChunk * (c + 1) : kBsChunk * c; };
-    auto load_chunk = [&](int c) {
-        const int px = clampi(chunk_base(c) + (sg >> 2), 0, W1 - 1);
+    for (int j = 0; j < kBsLPF; j++) cr[j] = *(const uint4*)(crow + (size_t)px(j) * 16);
+    uint32_t st[3] = {0u, 0u, 0u};
+    auto step = [&](int t, int j) {
+        const uint32_t cw[4] = {cr[j].x, cr[j].y, cr[j].z, cr[j].w};
+        uint32_t nw[3], dw[3];
+        bs_quad_step<P1, P2>(st, cw, fill_hi, fill_lo, odd, sh, nw, dw);
+        cr[j] = *(const uint4*)(crow + (size_t)px(t + kBsLPF) * 16);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 0; i < 16; i++) stg[i] = *(const uint4*)(lrow[i] + (size_t)px * 16);
+        for (int k = 0; k < 3; k++) st[k] = nw[k];
+        // unpredicated (lanes of rows past H repeat row H - 1)
+        uint32_t* o = drow + (size_t)px(t) * 12;
+        o[0] = dw[0];
+        o[1] = dw[1];
+        o[2] = dw[2];
     };
-    auto park_chunk = [&](int buf) {
-        unsigned char* b = lbuf + buf * kBsLineBufB + (lane >> 5) * kBsLineRowB + sg * 16;
+    // whole blocks without an exit inside (an exit per step would make the
+    // loop head wait for every load in flight), then the tail
+    int base = 0;
+    for (; base + kBsLPF <= W1; base += kBsLPF) {
 #pragma unroll
-        for (int i = 0; i < 16; i++) *(uint4*)(b + 2 * i * kBsLineRowB) = stg[i];
-    };
-    load_chunk(0);
-    park_chunk(0);
-    uint32_t sE[3] = {0u, 0u, 0u}, sO[3] = {0u, 0u, 0u};
-    const unsigned char* rbase = lbuf + rr * kBsLineRowB + h * 32;
-    for (int c = 0; c < nch; c++) {
-        if (c + 1 < nch) load_chunk(c + 1);
-        const unsigned char* cbuf = rbase + (c & 1) * kBsLineBufB;
-        const int b0 = chunk_base(c);
-#pragma unroll
-        for (int i = 0; i < kBsChunk; i++) {
-            const int st = kBsChunk * c + i;
-            if (st >= W1) break;
-            const int j = rl ? kBsChunk - 1 - i : i;
-            const uint4 e4 = *(const uint4*)(cbuf + j * 64), o4 = *(const uint4*)(cbuf + j * 64 + 16);
-            const uint32_t cE[4] = {e4.x, e4.y, e4.z, e4.w};
-            const uint32_t cO[4] = {o4.x, o4.y, o4.z, o4.w};
-            uint32_t nE[3], nO[3], dE[3], dO[3];
-            bs_dir_step<P1, P2>(sE, sO, cE, cO, fill0, fill1, nE, nO, dE, dO);
-#pragma unroll
-            for (int q = 0; q < 3; q++) {
-                sE[q] = nE[q];
-                sO[q] = nO[q];
-            }
-            // unpredicated (lanes of rows past H repeat row H - 1: same values at
-            // the same addresses)
-            uint2* o = (uint2*)(drow + (size_t)(b0 + j) * 12);
-            o[0] = make_uint2(dE[0], dE[1]);
-            o[1] = make_uint2(dE[2], dO[0]);
-            o[2] = make_uint2(dO[1], dO[2]);
-        }
-        if (c + 1 < nch) park_chunk((c + 1) & 1);
+        for (int j = 0; j < kBsLPF; j++) step(base + j, j);
     }
+#pragma unroll
+    for (int j = 0; j < kBsLPF; j++)
+        if (base + j < W1) step(base + j, j);
 }
 
 // ---------------------------------------------------------------------------
@@ -592,14 +606,12 @@ __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t*
             const int mC = Mv[pix];
             const int base = NDIR * (mC - e.P2);  // S = min(base + S', MAX_COST)
             const int bm = max(best - 1, 0), bp = min(best + 1, D - 1);
-            const int cb0 = min(bm & ~1, D - 4);
             const bool need = Sm >= clampS || Sp >= clampS;
-            const uint2 cw = *(const uint2*)(C + (need ? pix * D + cb0 : 0));
-            auto cword = [&](int d) -> int {
-                const int i = d - cb0;
-                const uint32_t wv = (i & 2) ? cw.y : cw.x;
-                return (int)((i & 1) ? (wv >> 16) : (wv & 0xffffu));
-            };
+            // C is stored [frame][y][x / 4][d][x % 4] on this pipeline (the
+            // cost kernel's bit-sliced mode, rows padded to 4 pixels)
+            const int prow = (int)(pix / W1), px = (int)(pix - (size_t)prow * W1);
+            const size_t cbase = ((size_t)prow * ((W1 + 3) & ~3) + (px & ~3)) * D + (px & 3);
+            auto cword = [&](int d) -> int { return need ? (int)(uint16_t)C[cbase + d * 4] : 0; };
             auto exact = [&](int Spp, int cv) -> int {
                 const int c1 = Spp >= clampS ? cv - mC : 0;
                 return min(base + Spp + NDIR * (c1 - min(c1, 2 * e.P2)), kMaxCost);
@@ -741,32 +753,35 @@ int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16
     }
     {
         StageTimer tm(ctx, kStagePath);
-        if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_fork, s), "fork")) ||
-            (rc = check_hip(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0), "fork wait")))
+        // the row directions after the strips on the context stream (default:
+        // the 8-frame step measured 3.58 ms this way against 3.67 ms with the
+        // lines beside the strips on the aux stream, MVSV_BS_SERIAL=0 -- the
+        // two slow each other down more than the strip chain's fill and drain
+        // leaves idle)
+        const bool side = !ctx->bs_serial;
+        if (side && ((rc = check_hip(ctx, hipEventRecord(ctx->ev_fork, s), "fork")) ||
+                     (rc = check_hip(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0), "fork wait"))))
             return rc;
-        // the row directions beside the strips (different units of work: the
-        // strip chain leaves SIMDs idle while it fills and drains); bs_serial:
-        // after them on the context stream (A/B, isolated stage times)
-        hipStream_t ls = ctx->bs_serial ? s : ctx->aux;
+        hipStream_t ls = side ? ctx->aux : s;
         auto lines = [&]() -> int {
             StageTimer tl(ctx, kStageLines, ls);
-            hipLaunchKernelGGL((bsgm_lines_kernel<2, 5>), dim3((H + 31) / 32, n, 2), dim3(64), 0, ls, Bv, Dv,
-                               dplane, H, e.W1, std::getenv("MVSV_BS_PROBE") ? 1 : 0);
+            hipLaunchKernelGGL((bsgm_lines4_kernel<2, 5>), dim3((H + 15) / 16, n, 2), dim3(64), 0, ls, Bv, Dv,
+                               dplane, H, e.W1);
             return check_hip(ctx, hipGetLastError(), "bit-sliced line kernel");
         };
-        if (!ctx->bs_serial && (rc = lines())) return rc;
+        if (side && (rc = lines())) return rc;
         {
             StageTimer ts(ctx, kStageStrips);
             const int ng = ctx->bs_groups;
             uint32_t* dummy = Dv + 2 * dplane;
             rc = ng == 1 ? launch_bs_strips<1>(ctx, n, H, e, Bv, Av, aplane, dummy)
-                 : ng == 4 ? launch_bs_strips<4>(ctx, n, H, e, Bv, Av, aplane, dummy)
-                           : launch_bs_strips<2>(ctx, n, H, e, Bv, Av, aplane, dummy);
+                 : ng == 2 ? launch_bs_strips<2>(ctx, n, H, e, Bv, Av, aplane, dummy)
+                           : launch_bs_strips<4>(ctx, n, H, e, Bv, Av, aplane, dummy);
             if (rc) return rc;
         }
-        if (ctx->bs_serial && (rc = lines())) return rc;
-        if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_join, ctx->aux), "join")) ||
-            (rc = check_hip(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0), "join wait")))
+        if (!side && (rc = lines())) return rc;
+        if (side && ((rc = check_hip(ctx, hipEventRecord(ctx->ev_join, ctx->aux), "join")) ||
+                     (rc = check_hip(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0), "join wait"))))
             return rc;
     }
     StageTimer tm(ctx, kStageFinal);

@@ -596,6 +596,9 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
     uint32_t* obase = (uint32_t*)C + (((size_t)f * H + y0) * W1 + x0 + tx0) * PP + p -
                       (size_t)(2 * SH2) * ostride;
     const int nout = min(kCost2Run, W1 - (x0 + tx0));
+    // the bit-sliced pipeline's pixel-quad-major C (D = 128: 16 uint4 per pixel)
+    const int W1q = (W1 + 3) & ~3;
+    uint4* cq = (uint4*)C + ((ptrdiff_t)((size_t)f * H + y0 - 2 * SH2) * W1q + x0 + tx0) * 16 + p;
     const bool hh_pin = e.fullDP != 0;  // the fix-up kernel's MODE_HH cases, done here
     const bool fix_x0 = (e.variant & MVSV_VARIANT_FIRSTCOL_FIX) != 0;
     const int ybot = max(H - SH2, 1);
@@ -659,9 +662,15 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                 // tile column): unpredicated stores
                 const bool full = __all(nout == kCost2Run);
                 if (emit) {
+                    bool done = false;
+                    // bit-sliced pipeline: C is stored pixel-quad major by the
+                    // C' block below (one 16-byte store per lane)
+                    if constexpr (PPC == 64) done = Bv != nullptr;
+                    if (!done) {
 #pragma unroll
-                    for (int i = 0; i < kCost2Run; i++)
-                        if (full || i < nout) orow[i * PP] = ov[i];
+                        for (int i = 0; i < kCost2Run; i++)
+                            if (full || i < nout) orow[i * PP] = ov[i];
+                    }
                 }
                 // residual plane + per-pixel minimum: the lanes of a column
                 // lane hold its pixel's D costs (PP <= 64 lanes, an aligned
@@ -714,10 +723,19 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                             const uint32_t r23 = pk_min_u16(sub2_nb(Plo23, B), p2x4) |
                                                  (pk_min_u16(sub2_nb(Phi23, B), p2x4) << 4);
                             const uint32_t tw = bs_transpose32(r01 | (r23 << 8), p);
-                            const int q = p & 31, k = q >> 3;
-                            const int c = ((k & 1) << 1) | (k >> 1);
+                            const int q = p & 31, kq = q >> 3;
+                            const int c = ((kq & 1) << 1) | (kq >> 1);
                             uint32_t* brow = Bv + (size_t)(orow - (uint32_t*)C) / PP * 16;
                             if (full || c < nout) brow[c * 16 + (p >> 5) * 8 + (q & 7)] = tw;
+                            // C is read only for the WTA's C(best -+ 1) gathers, so it
+                            // is stored [frame][y][x / 4][d][x % 4] (rows padded to
+                            // a multiple of 4 pixels, read by mvsv_bsgm.hip bsgm_wta_kernel):
+                            // the four pixels' C(d -+ 1) share a line; lane p writes
+                            // d = 2 p, 2 p + 1 of the wave's four columns -- the
+                            // wave's 1 KiB as one run
+                            // (a wave wholly right of W1 -- nout <= 0 -- would land in
+                            // the next row)
+                            if (nout > 0) cq[(ptrdiff_t)k * W1q * 16] = make_uint4(Plo01, Plo23, Phi01, Phi23);
                         }
                     }
                     if (Rv) {
@@ -3263,15 +3281,19 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     const size_t plane = (size_t)W * H;
     const size_t vol = (size_t)e.W1 * H * e.D;
     if ((rc = ensure(ctx, ctx->pre, (size_t)n * 2 * plane * 8, "sgbm BT interval planes"))) return rc;
-    if ((rc = ensure(ctx, ctx->cost, (size_t)n * vol * 2, "sgbm cost volume"))) return rc;
+    // (rows padded to a multiple of 4 pixels: the bit-sliced pipeline's layout)
+    if ((rc = ensure(ctx, ctx->cost, (size_t)n * H * ((e.W1 + 3) & ~3) * e.D * 2, "sgbm cost volume"))) return rc;
     // bit-sliced MODE_HH paths (round 5, mvsv_bsgm.hip): the cost kernel writes
     // the C' bit planes instead of the residual nibbles; the planes of the
     // direction passes are sized by bsgm_paths
-    const bool bs = bsgm_eligible(ctx, e, n, H) && ctx->path16 && ctx->tri && ctx->cost2 && ctx->cost_fixed_pp &&
-                    e.SH2 <= 7 && e.SW2 == e.SH2;
-    uint32_t* Bv = nullptr;
     // accumulator planes: one per concurrently written direction group
     const int sched = path_schedule(ctx, e, H, n);
+    // (launches too small to fill the GPU with strips -- one camera frame --
+    // keep the directions side by side: the bit-sliced passes trade fewer
+    // instructions for a longer serial chain per scanline)
+    const bool bs = bsgm_eligible(ctx, e, n, H) && sched == 1 && ctx->path16 && ctx->tri && ctx->cost2 &&
+                    ctx->cost_fixed_pp && e.SH2 <= 7 && e.SW2 == e.SH2;
+    uint32_t* Bv = nullptr;
     const int nplanes = sched == 2 ? (e.fullDP ? 7 : 4) : sched == 1 ? (e.fullDP ? 3 : 2) : 1;
     // 4-bit planes: one per direction (side by side, P2 <= 15) or per strip
     // pass + lines; bytes / u16 otherwise (side by side: one delta <= P2 each)

@@ -38,21 +38,28 @@ def test_bitslice_hh_forced(gpu, mvsv, oracle, case, bits):
               uniquenessRatio=0, speckleWindowSize=int(rng.choice([0, 20])), speckleRange=2, mode=1)
     variant = int(rng.integers(0, 4))
     try:
+        # single frames run the directions side by side unless the strip
+        # schedule is forced -- the schedule the bit-sliced path replaces
+        _lib.set_option(_lib.OPT_PATH_SCHEDULE, 1)
         _lib.set_option(_lib.OPT_BITSLICE, bits)
         got, want = sgbm_both(mvsv, oracle, L, R, variant=variant, **kw)
     finally:
         _lib.set_option(_lib.OPT_BITSLICE, 1)
+        _lib.set_option(_lib.OPT_PATH_SCHEDULE, 0)
     assert np.array_equal(got, want), f"bitslice={bits} variant={variant} {kw}: " + report(got, want)
 
 
-@pytest.mark.parametrize("groups", ["1", "2", "4"])
+@pytest.mark.parametrize("groups", ["1", "2", "4", "4-side"])
 def test_bitslice_strip_groups(gpu, mvsv, oracle, groups, monkeypatch):
-    """Every strip width (column groups per strip) on a 3-frame device batch."""
+    """Every strip width (column groups per strip) on a 3-frame device batch;
+    4-side: the line kernel beside the strips on the aux stream."""
     from mvstereovision3_amd import _lib
     torch = gpu
-    monkeypatch.setenv("MVSV_BS_GROUPS", groups)
+    monkeypatch.setenv("MVSV_BS_GROUPS", groups.split("-")[0])
+    monkeypatch.setenv("MVSV_BS_SERIAL", "0" if groups.endswith("side") else "1")
+    monkeypatch.setenv("MVSV_PATH_SCHEDULE", "1")
     ctx = _lib.Context(0)  # a fresh context reads the environment
-    rng = np.random.default_rng(5200 + int(groups))
+    rng = np.random.default_rng(5200 + len(groups) + int(groups[0]))
     H, W, D = 72, 330, 128
     pairs = [rand_pair(rng, H, W, int(rng.integers(0, 50)), k % 3) for k in range(3)]
     m = mvsv.StereoSGBM.create(minDisparity=1, numDisparities=D, blockSize=13, P1=0, P2=0, disp12MaxDiff=0,

@@ -19,7 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import kernel_source_sha  # noqa: E402
 
 STAGES = [("sgbm_tri_kernel", "path_strips"), ("bsgm_strip_kernel", "path_strips"),
-          ("bsgm_lines_kernel", "path_lines"), ("bsgm_wta_kernel", "final_wta_lr"),
+          ("bsgm_lines4_kernel", "path_lines"), ("bsgm_wta_kernel", "final_wta_lr"),
           ("sgbm_path16_kernel", "path_lines"),
           ("sgbm_path_kernel", "path_aggregation"), ("sgbm_cost_fixup", "cost_fixup"),
           ("sgbm_cost", "cost_volume"), ("sgbm_final", "final_wta_lr"),

@@ -35,7 +35,7 @@ SIMDS = 4 * CUS
 XCDS = 8
 
 STAGES = [("sgbm_tri_kernel", "path_strips"), ("bsgm_strip_kernel", "path_strips"),
-          ("bsgm_lines_kernel", "path_lines"), ("bsgm_wta_kernel", "final_wta_lr"),
+          ("bsgm_lines4_kernel", "path_lines"), ("bsgm_wta_kernel", "final_wta_lr"),
           ("sgbm_path16_kernel", "path_lines"),
           ("sgbm_pathdirs16_kernel", "path_aggregation"), ("sgbm_path_kernel", "path_aggregation"),
           ("sgbm_cost_fixup", "cost_fixup"), ("sgbm_cost", "cost_volume"),
