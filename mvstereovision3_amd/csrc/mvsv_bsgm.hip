@@ -154,6 +154,7 @@ struct BsStripCfg {
 // column 1), each 2 lanes x 6 words; one u64 granule = 32-bit launch tag | word
 constexpr int kBsGran = 36;
 constexpr int kBsPF = 4;  // steps of C' prefetch (compute waves)
+constexpr int kBsStripLds = 96 * 1024;  // strip block LDS allocation (launch_bs_strips)
 constexpr int kBsBF = 4;  // steps of boundary prefetch (exchange wave)
 
 template <int NG, int P1, int P2>
@@ -447,11 +448,11 @@ __global__ __launch_bounds__(BsStripCfg<NG>::kThreads) void bsgm_strip_kernel(
 // loads its own 16 bytes kBsLPF steps ahead into registers (a load instruction
 // covers 16 rows x one 64-byte record): the pass is bound by the memory
 // parallelism of its few waves, not by their instructions.
-constexpr int kBsLPF = 16;
+constexpr int kBsLPF = 32;
 
 template <int P1, int P2>
 __global__ __launch_bounds__(64) void bsgm_lines4_kernel(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dl,
-                                                          size_t plane_words, int H, int W1)
+                                                          size_t plane_words, int H, int W1, int probe)
 {
     const int lane = threadIdx.x;
     const int q = lane & 3, rr = lane >> 2;
@@ -465,20 +466,21 @@ __global__ __launch_bounds__(64) void bsgm_lines4_kernel(const uint32_t* __restr
     const uint32_t* crow = Bc + rowpix * 16 + q * 4;
     // pixel of step t (clamped: loads past the row's end are issued, not used)
     auto px = [&](int t) { return rl ? max(W1 - 1 - t, 0) : min(t, W1 - 1); };
+    auto lpx = [&](int t) { return (probe & 2) ? (t & 7) : px(t); };
     uint4 cr[kBsLPF];
 #pragma unroll
-    for (int j = 0; j < kBsLPF; j++) cr[j] = *(const uint4*)(crow + (size_t)px(j) * 16);
+    for (int j = 0; j < kBsLPF; j++) cr[j] = *(const uint4*)(crow + (size_t)lpx(j) * 16);
     uint32_t st[3] = {0u, 0u, 0u};
     auto step = [&](int t, int j) {
         const uint32_t cw[4] = {cr[j].x, cr[j].y, cr[j].z, cr[j].w};
         uint32_t nw[3], dw[3];
         bs_quad_step<P1, P2>(st, cw, fill_hi, fill_lo, odd, sh, nw, dw);
-        cr[j] = *(const uint4*)(crow + (size_t)px(t + kBsLPF) * 16);
+        cr[j] = *(const uint4*)(crow + (size_t)lpx(t + kBsLPF) * 16);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = 0; k < 3; k++) st[k] = nw[k];
         // unpredicated (lanes of rows past H repeat row H - 1)
-        uint32_t* o = drow + (size_t)px(t) * 12;
+        uint32_t* o = drow + (size_t)((probe & 1) ? 0 : px(t)) * 12;
         o[0] = dw[0];
         o[1] = dw[1];
         o[2] = dw[2];
@@ -700,12 +702,20 @@ static int launch_bs_strips(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const
         (void)hipMemset(stats, 0, (size_t)grid.x * 64);
     }
     const bool nowait = std::getenv("MVSV_BS_NOWAIT") != nullptr;
-    if (Cfg::kBytes > 65536 &&
+    // one strip block per CU: dynamic LDS past half the CU's 160 KiB (a second
+    // strip block on the same CU makes that CU's strips, and every strip left of
+    // them in the chain, step at half speed -- 2-group strips measured 1.17 ms
+    // two to a CU, 0.88 ms one to a CU, 4-group strips 0.98 ms either way;
+    // the lines / cost blocks of a concurrent batch still fit beside it).
+    // MVSV_BS_LDSPAD overrides the size (A/B).
+    size_t lds = std::max(Cfg::kBytes, (size_t)kBsStripLds);
+    if (const char* pv = std::getenv("MVSV_BS_LDSPAD")) lds = std::max(Cfg::kBytes, (size_t)std::atol(pv));
+    if (lds > 65536 &&
         (rc = check_hip(ctx, hipFuncSetAttribute((const void*)bsgm_strip_kernel<NG, 2, 5>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::kBytes),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                         "bit-sliced strip LDS attribute")))
         return rc;
-    hipLaunchKernelGGL((bsgm_strip_kernel<NG, 2, 5>), grid, dim3(Cfg::kThreads), Cfg::kBytes, ctx->stream, Bv, Av,
+    hipLaunchKernelGGL((bsgm_strip_kernel<NG, 2, 5>), grid, dim3(Cfg::kThreads), lds, ctx->stream, Bv, Av,
                        aplane, dummy, H, e.W1, npass, (unsigned long long*)ctx->bs_bnd.ptr, epoch, n,
                        (int*)ctx->status.ptr, ctx->spin_limit, ctx->report_target,
                        tickets ? (long long)ctx->tri_tickets : -1ll, stats, nowait ? 1 : 0);
@@ -765,8 +775,9 @@ int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16
         hipStream_t ls = side ? ctx->aux : s;
         auto lines = [&]() -> int {
             StageTimer tl(ctx, kStageLines, ls);
+            const char* pv = std::getenv("MVSV_BS_LPROBE");
             hipLaunchKernelGGL((bsgm_lines4_kernel<2, 5>), dim3((H + 15) / 16, n, 2), dim3(64), 0, ls, Bv, Dv,
-                               dplane, H, e.W1);
+                               dplane, H, e.W1, pv ? std::atoi(pv) : 0);
             return check_hip(ctx, hipGetLastError(), "bit-sliced line kernel");
         };
         if (side && (rc = lines())) return rc;
@@ -774,9 +785,10 @@ int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16
             StageTimer ts(ctx, kStageStrips);
             const int ng = ctx->bs_groups;
             uint32_t* dummy = Dv + 2 * dplane;
-            rc = ng == 1 ? launch_bs_strips<1>(ctx, n, H, e, Bv, Av, aplane, dummy)
-                 : ng == 2 ? launch_bs_strips<2>(ctx, n, H, e, Bv, Av, aplane, dummy)
-                           : launch_bs_strips<4>(ctx, n, H, e, Bv, Av, aplane, dummy);
+            rc = ng == 1   ? launch_bs_strips<1>(ctx, n, H, e, Bv, Av, aplane, dummy)
+                 : ng == 4 ? launch_bs_strips<4>(ctx, n, H, e, Bv, Av, aplane, dummy)
+                 : ng == 5 ? launch_bs_strips<5>(ctx, n, H, e, Bv, Av, aplane, dummy)
+                           : launch_bs_strips<2>(ctx, n, H, e, Bv, Av, aplane, dummy);
             if (rc) return rc;
         }
         if (!side && (rc = lines())) return rc;

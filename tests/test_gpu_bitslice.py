@@ -49,7 +49,7 @@ def test_bitslice_hh_forced(gpu, mvsv, oracle, case, bits):
     assert np.array_equal(got, want), f"bitslice={bits} variant={variant} {kw}: " + report(got, want)
 
 
-@pytest.mark.parametrize("groups", ["1", "2", "4", "4-side"])
+@pytest.mark.parametrize("groups", ["1", "2", "4", "5", "2-side"])
 def test_bitslice_strip_groups(gpu, mvsv, oracle, groups, monkeypatch):
     """Every strip width (column groups per strip) on a 3-frame device batch;
     4-side: the line kernel beside the strips on the aux stream."""

@@ -60,6 +60,67 @@ __device__ __forceinline__ void step(uint32_t (&sE)[3], uint32_t (&sO)[3], const
     for (int k = 0; k < 3; k++) acc[k] ^= dE[k] ^ dO[k];
 }
 
+// the lane-quad form (mvsv_bsgm.hip bs_quad_step)
+template <int P1, int P2>
+__device__ __forceinline__ void qstep(uint32_t (&s)[3], const uint32_t (&c)[4], uint32_t fill_hi, uint32_t fill_lo,
+                                      bool odd, uint32_t sh, uint32_t (&acc)[3])
+{
+    uint32_t nb[3], pt[3], d[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)s[k], 0xF9, 0xf, 0xf, true) | fill_hi;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)s[k], 0x90, 0xf, 0xf, true) | fill_lo;
+        nb[k] = __builtin_amdgcn_alignbit(hi, lo, sh);
+        pt[k] = odd ? lo : hi;
+    }
+    delta3<P1, P2>(s, nb, pt, d);
+    uint32_t v[4];
+    add43(c, d, v);
+    uint32_t kk = ~v[3], M[3];
+#pragma unroll
+    for (int b = 2; b >= 0; b--) {
+        const uint32_t z = lop3<kAndNotAB>(v[b], kk, kk);
+        uint32_t any = z | xswap(z);
+        any |= (uint32_t)__builtin_amdgcn_mov_dpp((int)any, 0x4E, 0xf, 0xf, true);
+        const bool f = any != 0u;
+        if (b > 0) kk = f ? z : kk;
+        M[b] = f ? 0u : 0xffffffffu;
+    }
+    subclamp<P2>(v, M[0], M[1], M[2], s);
+#pragma unroll
+    for (int k = 0; k < 3; k++) acc[k] ^= d[k];
+}
+
+template <int ILP>
+__global__ void qchain(const uint32_t* seed, uint32_t* out, unsigned long long* clk)
+{
+    const int lane = threadIdx.x & 63, q = lane & 3;
+    const bool odd = q & 1;
+    const uint32_t fill_hi = q == 3 ? 0xffffffffu : 0u, fill_lo = q == 0 ? 0xffffffffu : 0u, sh = odd ? 1u : 31u;
+    uint32_t s[ILP][3], c[ILP][4], acc[ILP][3];
+    for (int i = 0; i < ILP; i++) {
+        for (int k = 0; k < 3; k++) s[i][k] = acc[i][k] = 0;
+        for (int k = 0; k < 4; k++) c[i][k] = seed[(lane * 8 + k + i) & 255];
+        c[i][3] = 0;
+    }
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int t = 0; t < STEPS; t++) {
+#pragma unroll
+        for (int i = 0; i < ILP; i++) {
+            qstep<2, 5>(s[i], c[i], fill_hi, fill_lo, odd, sh, acc[i]);
+#pragma unroll
+            for (int k = 0; k < 3; k++) c[i][k] = __builtin_amdgcn_alignbit(c[i][k], c[i][k], 7);
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    uint32_t r = 0;
+    for (int i = 0; i < ILP; i++)
+        for (int k = 0; k < 3; k++) r ^= acc[i][k] ^ s[i][k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+    if (threadIdx.x % 64 == 0) clk[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
+}
+
 template <int ILP>
 __global__ void chain(const uint32_t* seed, uint32_t* out, unsigned long long* clk)
 {
@@ -97,7 +158,7 @@ __global__ void chain(const uint32_t* seed, uint32_t* out, unsigned long long* c
     if (threadIdx.x % 64 == 0) clk[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
 }
 
-template <int ILP>
+template <int ILP, bool Q = false>
 static void run(int waves_per_simd)
 {
     const int threads = 256 * waves_per_simd;  // 4 SIMDs per CU
@@ -111,13 +172,14 @@ static void run(int waves_per_simd)
     hipMemcpy(seed, hs.data(), 256 * 4, hipMemcpyHostToDevice);
     hipMalloc(&out, (size_t)blocks * threads * 4);
     hipMalloc(&clk, (size_t)blocks * threads / 64 * 8);
-    hipLaunchKernelGGL(chain<ILP>, dim3(blocks), dim3(threads), 0, 0, seed, out, clk);
+    auto kern = Q ? qchain<ILP> : chain<ILP>;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, seed, out, clk);
     hipDeviceSynchronize();
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
     hipEventRecord(a);
-    hipLaunchKernelGGL(chain<ILP>, dim3(blocks), dim3(threads), 0, 0, seed, out, clk);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, seed, out, clk);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms = 0;
@@ -127,9 +189,9 @@ static void run(int waves_per_simd)
     double mean = 0;
     for (auto v : c) mean += (double)v;
     mean /= c.size();
-    std::printf("ILP %d, %d waves/SIMD: %.1f shader cycles per step per wave (%.1f per pixel-step per SIMD), "
+    std::printf("%s ILP %d, %d waves/SIMD: %.1f shader cycles per step per wave (%.1f per pixel-step per SIMD), "
                 "kernel %.3f ms\n",
-                ILP, waves_per_simd, mean / STEPS, mean / STEPS / (ILP * waves_per_simd), ms);
+                Q ? "quad" : "pair", ILP, waves_per_simd, mean / STEPS, mean / STEPS / (ILP * waves_per_simd), ms);
     hipFree(seed);
     hipFree(out);
     hipFree(clk);
@@ -140,7 +202,8 @@ int main()
     for (int w : {1, 2, 4}) {
         run<1>(w);
         run<2>(w);
-        run<4>(w);
+        run<1, true>(w);
+        run<2, true>(w);
     }
     return 0;
 }
