@@ -17,6 +17,7 @@
 // scalar recurrence); the cross-lane steps live in the kernels.
 #pragma once
 
+#include <stddef.h>
 #include <stdint.h>
 
 #if defined(__HIPCC__)
@@ -183,6 +184,15 @@ MVSV_BS_HD void subclamp(const uint32_t (&v)[4], uint32_t m0, uint32_t m1, uint3
     s[1] = (P2 & 2) ? (r1 | ge) : lop3<(kA & ~kB) & 0xFFu>(r1, ge, ge);
     s[2] = (P2 & 4) ? (r2 | ge) : lop3<(kA & ~kB) & 0xFFu>(r2, ge, ge);
 }
+
+// Plane layouts of the pipeline (rows padded to W1q = W1 rounded up to 4
+// pixels; rowq = (frame * H + y) * W1q).  The C' plane groups four pixels:
+// [x / 4][q][x % 4][bit b] with q = 2 h + e, so a lane that owns one (h, e)
+// word set of a row reads 64 contiguous bytes per four pixels; the line delta
+// planes likewise [x / 4][q][x % 4][b < 3].
+MVSV_BS_HD size_t cq_word(size_t rowq, int x, int q) { return (rowq + (size_t)(x & ~3)) * 16 + q * 16 + (x & 3) * 4; }
+MVSV_BS_HD size_t dl_word(size_t rowq, int x, int q) { return (rowq + (size_t)(x & ~3)) * 12 + q * 12 + (x & 3) * 3; }
+MVSV_BS_HD int padq(int w) { return (w + 3) & ~3; }
 
 // scalar value of a sliced number at word bit p (host checks, sub-pixel reads)
 template <int NB>

@@ -278,6 +278,13 @@ __global__ __launch_bounds__(BsStripCfg<NG>::kThreads) void bsgm_strip_kernel(
     const int cst = (rowW + 1) * 16;
     const int fbase = f * H * W1 * 16 + h * 8;
     auto cell_off = [&](int t) -> int { return (unsigned)cell_x(t) < (unsigned)W1 ? c0 + t * cst : fbase; };
+    // the cell's E words in the grouped C' plane (bs::cq_word, q = 2 h); O at + 16
+    const int W1q = bs::padq(W1);
+    auto c_off = [&](int t) -> int {
+        const int x = cell_x(t);
+        if ((unsigned)x >= (unsigned)W1) return f * H * W1q * 16 + h * 32;
+        return (int)bs::cq_word((size_t)(f * H + (sy > 0 ? t : H - 1 - t)) * W1q, x, 2 * h);
+    };
     uint32_t* Ap = A + (size_t)pass * plane_words;
     uint4 cb[kBsPF][2];
     uint32_t sa[6];  // direction a's state (E words 0..2, O words 3..5)
@@ -296,9 +303,9 @@ __global__ __launch_bounds__(BsStripCfg<NG>::kThreads) void bsgm_strip_kernel(
     } else {
 #pragma unroll
         for (int j = 0; j < kBsPF; j++) {
-            const uint4* q = (const uint4*)(Bc + cell_off(min(tb + j, te - 1)));
+            const uint4* q = (const uint4*)(Bc + c_off(min(tb + j, te - 1)));
             cb[j][0] = q[0];
-            cb[j][1] = q[1];
+            cb[j][1] = q[4];
         }
     }
     __syncthreads();
@@ -364,9 +371,9 @@ __global__ __launch_bounds__(BsStripCfg<NG>::kThreads) void bsgm_strip_kernel(
         bs_dir_step<P1, P2>(sE, sO, cE, cO, fill0, fill1, nE, nO, dE, dO);
         {
             // the slot's next load once its words are consumed (same registers)
-            const uint4* q = (const uint4*)(Bc + cell_off(min(t + kBsPF, te - 1)));
+            const uint4* q = (const uint4*)(Bc + c_off(min(t + kBsPF, te - 1)));
             cb[j][0] = q[0];
-            cb[j][1] = q[1];
+            cb[j][1] = q[4];
             __builtin_amdgcn_sched_barrier(0);
         }
         if (!valid) {
@@ -442,13 +449,14 @@ __global__ __launch_bounds__(BsStripCfg<NG>::kThreads) void bsgm_strip_kernel(
 // Lines: L->R (blockIdx.z = 0) and R->L (1); each writes its delta plane (3 bits).
 // ---------------------------------------------------------------------------
 // The lines on lane quads (bs_quad_step): 16 rows per wave, lane 4 r + q holds
-// words (h, e) = (q >> 1, q & 1) of row r -- 16 contiguous bytes of the C'
-// record and 12 of the delta record -- so the grid has twice the waves of a
-// lane-pair layout at two thirds of the instructions per step.  Each lane
-// loads its own 16 bytes kBsLPF steps ahead into registers (a load instruction
-// covers 16 rows x one 64-byte record): the pass is bound by the memory
-// parallelism of its few waves, not by their instructions.
-constexpr int kBsLPF = 32;
+// words (h, e) = (q >> 1, q & 1) of row r, so the grid has twice the waves of a
+// lane-pair layout at two thirds of the instructions per step.  The planes are
+// grouped by four pixels (bs::cq_word / dl_word): per four steps a lane loads 64
+// contiguous bytes of C' (kBsLG groups ahead, in registers) and stores 48 of
+// deltas -- with one 16-byte load and one 12-byte store per step (a load
+// instruction then covering 16 rows x 64 bytes) the pass measured 0.50 ms of
+// which 0.28 went to those loads and 0.14 to those stores (MVSV_BS_LPROBE).
+constexpr int kBsLG = 8;
 
 template <int P1, int P2>
 __global__ __launch_bounds__(64) void bsgm_lines4_kernel(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dl,
@@ -458,43 +466,95 @@ __global__ __launch_bounds__(64) void bsgm_lines4_kernel(const uint32_t* __restr
     const int q = lane & 3, rr = lane >> 2;
     const int y = min((int)blockIdx.x * 16 + rr, H - 1);
     const int f = blockIdx.y;
-    const bool rl = blockIdx.z != 0;
     const bool odd = (q & 1) != 0;
     const uint32_t fill_hi = q == 3 ? kOnes : 0u, fill_lo = q == 0 ? kOnes : 0u, sh = odd ? 1u : 31u;
-    const size_t rowpix = (size_t)(f * H + y) * W1;
-    uint32_t* drow = Dl + (rl ? plane_words : 0) + rowpix * 12 + q * 3;
-    const uint32_t* crow = Bc + rowpix * 16 + q * 4;
-    // pixel of step t (clamped: loads past the row's end are issued, not used)
-    auto px = [&](int t) { return rl ? max(W1 - 1 - t, 0) : min(t, W1 - 1); };
-    auto lpx = [&](int t) { return (probe & 2) ? (t & 7) : px(t); };
-    uint4 cr[kBsLPF];
+    const size_t rowq = (size_t)(f * H + y) * bs::padq(W1);
+    // group g's 64 bytes of this lane / its 48 delta bytes
+    const uint4* cgrp = (const uint4*)(Bc + bs::cq_word(rowq, 0, q));
+    const int G = (W1 + 3) >> 2;
+    const int part = W1 & 3;
+    auto run = [&](auto rltag) __attribute__((always_inline)) {
+        constexpr bool RL = decltype(rltag)::value;
+        uint4* dgrp = (uint4*)(Dl + (RL ? plane_words : 0) + bs::dl_word(rowq, 0, q));
+        // group of the i-th group step (clamped: loads past the row are issued, not used)
+        auto grp = [&](int i) { return RL ? max(G - 1 - i, 0) : min(i, G - 1); };
+        auto lgrp = [&](int i) { return (probe & 2) ? (i & 1) : grp(i); };
+        uint4 cr[kBsLG][4];
+        auto load = [&](int j, int i) {
+            const uint4* p = cgrp + (size_t)lgrp(i) * 16;
 #pragma unroll
-    for (int j = 0; j < kBsLPF; j++) cr[j] = *(const uint4*)(crow + (size_t)lpx(j) * 16);
-    uint32_t st[3] = {0u, 0u, 0u};
-    auto step = [&](int t, int j) {
-        const uint32_t cw[4] = {cr[j].x, cr[j].y, cr[j].z, cr[j].w};
-        uint32_t nw[3], dw[3];
-        bs_quad_step<P1, P2>(st, cw, fill_hi, fill_lo, odd, sh, nw, dw);
-        cr[j] = *(const uint4*)(crow + (size_t)lpx(t + kBsLPF) * 16);
-        __builtin_amdgcn_sched_barrier(0);
+            for (int u = 0; u < 4; u++) cr[j][u] = p[u];
+        };
+        // R->L with a partial group: that group (step 0) first, from its own
+        // registers; ring slot j then holds group steps ph + j + kBsLG m
+        const int ph = (RL && part) ? 1 : 0;
+        uint4 c0[4];
+        if (ph) {
 #pragma unroll
-        for (int k = 0; k < 3; k++) st[k] = nw[k];
-        // unpredicated (lanes of rows past H repeat row H - 1)
-        uint32_t* o = drow + (size_t)((probe & 1) ? 0 : px(t)) * 12;
-        o[0] = dw[0];
-        o[1] = dw[1];
-        o[2] = dw[2];
+            for (int u = 0; u < 4; u++) c0[u] = cgrp[(size_t)lgrp(0) * 16 + u];
+        }
+        // (issued in slot order: the loop head's wait for slot 0 assumes it)
+#pragma unroll
+        for (int j = 0; j < kBsLG; j++) {
+            load(j, ph + j);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        uint32_t st[3] = {0u, 0u, 0u};
+        // the pixels x = 4 g + u of group step i (u descending for R->L); n < 4:
+        // the row's partial group (x >= W1 skipped: the state must not advance)
+        auto group = [&](int i, uint4 (&cg)[4], int n) {
+            uint32_t dv[12];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int u = RL ? 3 - k : k;
+                if (u < n) {
+                    const uint32_t cw[4] = {cg[u].x, cg[u].y, cg[u].z, cg[u].w};
+                    uint32_t nw[3], dw[3];
+                    bs_quad_step<P1, P2>(st, cw, fill_hi, fill_lo, odd, sh, nw, dw);
+#pragma unroll
+                    for (int b = 0; b < 3; b++) {
+                        st[b] = nw[b];
+                        dv[3 * u + b] = dw[b];
+                    }
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 3; b++) dv[3 * u + b] = 0u;
+                }
+            }
+            uint4* o = dgrp + (size_t)((probe & 1) ? 0 : grp(i)) * 12;
+            o[0] = make_uint4(dv[0], dv[1], dv[2], dv[3]);
+            o[1] = make_uint4(dv[4], dv[5], dv[6], dv[7]);
+            o[2] = make_uint4(dv[8], dv[9], dv[10], dv[11]);
+        };
+        // a ring group: compute, then reload its slot kBsLG group steps ahead
+        auto ring = [&](int i, int j, int n) {
+            group(i, cr[j], n);
+            load(j, i + kBsLG);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        // the partial group (W1 % 4 pixels) is the last for L->R and the first
+        // for R->L.  Whole blocks of kBsLG groups without exits in between (an
+        // exit per group would make the loop head wait for every load in flight)
+        if (ph) group(0, c0, part);
+        const int full_end = (RL || !part) ? G : G - 1;
+        int i = ph;
+        for (; i + kBsLG <= full_end; i += kBsLG) {
+#pragma unroll
+            for (int j = 0; j < kBsLG; j++) ring(i + j, j, 4);
+        }
+        // tail: full groups, then L->R's partial group (slot full_end - i)
+#pragma unroll
+        for (int j = 0; j < kBsLG; j++) {
+            if (i + j < full_end)
+                ring(i + j, j, 4);
+            else if (i + j == full_end && !RL && part)
+                ring(i + j, j, part);
+        }
     };
-    // whole blocks without an exit inside (an exit per step would make the
-    // loop head wait for every load in flight), then the tail
-    int base = 0;
-    for (; base + kBsLPF <= W1; base += kBsLPF) {
-#pragma unroll
-        for (int j = 0; j < kBsLPF; j++) step(base + j, j);
-    }
-#pragma unroll
-    for (int j = 0; j < kBsLPF; j++)
-        if (base + j < W1) step(base + j, j);
+    if (blockIdx.z != 0)
+        run(std::true_type());
+    else
+        run(std::false_type());
 }
 
 // ---------------------------------------------------------------------------
@@ -537,25 +597,28 @@ __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t*
         const size_t pix = pix0 + x;
         uint32_t c[2][4], ad[2][4], au[2][4], dl[2][3], dr[2][3];
         {
-            const uint4* qc = (const uint4*)(Bc + pix * 16 + h * 8);
+            // grouped C' and line planes (bs::cq_word / dl_word), E then O
+            const size_t rowq = (size_t)(f * H + y) * bs::padq(W1);
+            const uint32_t* qc = Bc + bs::cq_word(rowq, x, 2 * h);
             const uint4* qd = (const uint4*)(A + pix * 16 + h * 8);
             const uint4* qu = (const uint4*)(A + aplane + pix * 16 + h * 8);
-            const uint2* ql = (const uint2*)(Dl + pix * 12 + h * 6);
-            const uint2* qr = (const uint2*)(Dl + dplane + pix * 12 + h * 6);
+            const uint32_t* ql = Dl + bs::dl_word(rowq, x, 2 * h);
+            const uint32_t* qr = Dl + dplane + bs::dl_word(rowq, x, 2 * h);
             uint4 t;
 #pragma unroll
             for (int e2 = 0; e2 < 2; e2++) {
-                t = qc[e2];
+                t = *(const uint4*)(qc + 16 * e2);
                 c[e2][0] = t.x, c[e2][1] = t.y, c[e2][2] = t.z, c[e2][3] = t.w;
                 t = qd[e2];
                 ad[e2][0] = t.x, ad[e2][1] = t.y, ad[e2][2] = t.z, ad[e2][3] = t.w;
                 t = qu[e2];
                 au[e2][0] = t.x, au[e2][1] = t.y, au[e2][2] = t.z, au[e2][3] = t.w;
+#pragma unroll
+                for (int b = 0; b < 3; b++) {
+                    dl[e2][b] = ql[12 * e2 + b];
+                    dr[e2][b] = qr[12 * e2 + b];
+                }
             }
-            const uint2 l0 = ql[0], l1 = ql[1], l2 = ql[2];
-            const uint2 r0 = qr[0], r1 = qr[1], r2 = qr[2];
-            dl[0][0] = l0.x, dl[0][1] = l0.y, dl[0][2] = l1.x, dl[1][0] = l1.y, dl[1][1] = l2.x, dl[1][2] = l2.y;
-            dr[0][0] = r0.x, dr[0][1] = r0.y, dr[0][2] = r1.x, dr[1][0] = r1.y, dr[1][1] = r2.x, dr[1][2] = r2.y;
         }
         uint32_t S[2][7];
 #pragma unroll
@@ -666,7 +729,7 @@ bool bsgm_eligible(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H)
            e.W1 > 0 && (size_t)n * H * e.W1 * 16 < ((size_t)1 << 31);
 }
 
-size_t bsgm_plane_bytes(int n, int H, int W1) { return (size_t)n * H * W1 * 64; }
+size_t bsgm_plane_bytes(int n, int H, int W1) { return (size_t)n * H * bs::padq(W1) * 64; }
 
 template <int NG>
 static int launch_bs_strips(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const uint32_t* Bv, uint32_t* Av,
@@ -748,7 +811,7 @@ int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16
 {
     int rc;
     const size_t aplane = (size_t)n * H * e.W1 * 16;  // words per strip-pass plane
-    const size_t dplane = (size_t)n * H * e.W1 * 12;  // words per line plane
+    const size_t dplane = (size_t)n * H * bs::padq(e.W1) * 12;  // words per line plane (grouped, padded rows)
     // + 512 words: the strip kernel's dummy store slots (cells outside the image)
     if ((rc = ensure(ctx, ctx->agg, (2 * aplane + 2 * dplane + 512) * 4, "bit-sliced delta planes"))) return rc;
     if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
@@ -763,11 +826,11 @@ int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16
     }
     {
         StageTimer tm(ctx, kStagePath);
-        // the row directions after the strips on the context stream (default:
-        // the 8-frame step measured 3.58 ms this way against 3.67 ms with the
-        // lines beside the strips on the aux stream, MVSV_BS_SERIAL=0 -- the
-        // two slow each other down more than the strip chain's fill and drain
-        // leaves idle)
+        // the row directions beside the strips on the aux stream (the strip
+        // chain leaves CUs idle while it fills and drains, the line waves are
+        // few and memory-bound): bench 2970 vs 2850 Mpix/s with the lines after
+        // the strips on the context stream (MVSV_BS_SERIAL=1, same box, with
+        // one-block-per-CU 2-group strips and the grouped planes)
         const bool side = !ctx->bs_serial;
         if (side && ((rc = check_hip(ctx, hipEventRecord(ctx->ev_fork, s), "fork")) ||
                      (rc = check_hip(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0), "fork wait"))))

@@ -599,6 +599,8 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
     // the bit-sliced pipeline's pixel-quad-major C (D = 128: 16 uint4 per pixel)
     const int W1q = (W1 + 3) & ~3;
     uint4* cq = (uint4*)C + ((ptrdiff_t)((size_t)f * H + y0 - 2 * SH2) * W1q + x0 + tx0) * 16 + p;
+    // ... and the C' bit planes' four-pixel group of the wave's columns
+    uint32_t* bq = Bv ? Bv + ((ptrdiff_t)((size_t)f * H + y0 - 2 * SH2) * W1q + x0 + tx0) * 16 : nullptr;
     const bool hh_pin = e.fullDP != 0;  // the fix-up kernel's MODE_HH cases, done here
     const bool fix_x0 = (e.variant & MVSV_VARIANT_FIRSTCOL_FIX) != 0;
     const int ybot = max(H - SH2, 1);
@@ -725,8 +727,10 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                             const uint32_t tw = bs_transpose32(r01 | (r23 << 8), p);
                             const int q = p & 31, kq = q >> 3;
                             const int c = ((kq & 1) << 1) | (kq >> 1);
-                            uint32_t* brow = Bv + (size_t)(orow - (uint32_t*)C) / PP * 16;
-                            if (full || c < nout) brow[c * 16 + (p >> 5) * 8 + (q & 7)] = tw;
+                            // the four-pixel group of the wave's columns (mvsv_bitslice.hpp
+                            // cq_word): word (q' = 2 h + e) * 16 + c * 4 + b
+                            const int qw = (2 * (p >> 5) + ((q & 7) >> 2)) * 16 + c * 4 + (q & 3);
+                            if (full || c < nout) bq[(ptrdiff_t)k * W1q * 16 + qw] = tw;
                             // C is read only for the WTA's C(best -+ 1) gathers, so it
                             // is stored [frame][y][x / 4][d][x % 4] (rows padded to
                             // a multiple of 4 pixels, read by mvsv_bsgm.hip bsgm_wta_kernel):

@@ -4,7 +4,8 @@
 // recurrence -- two lanes per pixel (64-disparity halves), E / O parity words,
 // the neighbour words through the partner lane, the bit-serial row minimum --
 // against OpenCV 3.4's recurrence on unclamped costs, the
-// cost kernel's 32 x 32 lane transpose against its definition, and the WTA
+// lane-quad form of the step (the line kernel's), the grouped plane layouts,
+// the cost kernel's 32 x 32 lane transpose against its definition, and the WTA
 // sum / argmin / neighbour extraction of the bit-sliced final pass.
 #include <cstdint>
 #include <cstdio>
@@ -162,6 +163,41 @@ static void pair_step(Lane (&ln)[2], const uint32_t (&cE)[2][4], const uint32_t 
     }
 }
 
+// The lane-quad step (bs_quad_step in mvsv_bsgm.hip): lane q = 2 h + e holds
+// the parity-e words of half h; the shifted neighbour is alignbit(hi = quad
+// lane q + 1, lo = q - 1) by 1 (odd) / 31 (even), all-ones past the quad's
+// ends, the partner word is lo (odd) / hi (even), the minimum ORs the quad.
+static void quad_step(uint32_t (&s)[4][3], const uint32_t (&c)[4][4], uint32_t (&d)[4][3])
+{
+    uint32_t v[4][4];
+    for (int q = 0; q < 4; q++) {
+        const bool odd = (q & 1) != 0;
+        uint32_t nb[3], pt[3];
+        for (int k = 0; k < 3; k++) {
+            const uint32_t hi = q < 3 ? s[q + 1][k] : ONES;
+            const uint32_t lo = q > 0 ? s[q - 1][k] : ONES;
+            nb[k] = fshr(hi, lo, odd ? 1 : 31);
+            pt[k] = odd ? lo : hi;
+        }
+        delta3<P1, P2>(s[q], nb, pt, d[q]);
+        add43(c[q], d[q], v[q]);
+    }
+    uint32_t kk[4], M[3];
+    for (int q = 0; q < 4; q++) kk[q] = ~v[q][3];
+    for (int b = 2; b >= 0; b--) {
+        uint32_t z[4], any = 0;
+        for (int q = 0; q < 4; q++) {
+            z[q] = kk[q] & ~v[q][b];
+            any |= z[q];
+        }
+        const bool f = any != 0u;
+        if (b > 0 && f)
+            for (int q = 0; q < 4; q++) kk[q] = z[q];
+        M[b] = f ? 0u : ONES;
+    }
+    for (int q = 0; q < 4; q++) subclamp<P2>(v[q], M[0], M[1], M[2], s[q]);
+}
+
 static int dof(int h, int e, int p) { return 64 * h + 2 * p + e; }
 
 static void check_recurrence(std::mt19937& rng)
@@ -172,6 +208,7 @@ static void check_recurrence(std::mt19937& rng)
         // scalar state (OpenCV's L - the unbiased cost of the first step)
         std::vector<int> Lp(D, 0);
         Lane ln[2] = {};
+        uint32_t sq[4][3] = {};  // the lane-quad form of the same scanline
         const int mode = line % 4;  // cost distributions: wide, narrow, flat, spiky
         for (int i = 0; i < N; i++) {
             int C[D];
@@ -186,6 +223,7 @@ static void check_recurrence(std::mt19937& rng)
             if (i % 17 == 16) {  // a path restart: state of an out-of-image predecessor is 0
                 std::fill(Lp.begin(), Lp.end(), 0);
                 ln[0] = ln[1] = Lane{};
+                for (auto& w : sq) w[0] = w[1] = w[2] = 0u;
             }
             int minLp = 1 << 30;
             for (int d = 0; d < D; d++) minLp = std::min(minLp, Lp[d]);
@@ -208,6 +246,17 @@ static void check_recurrence(std::mt19937& rng)
                 }
             uint32_t dE[2][3], dO[2][3];
             pair_step(ln, cE, cO, dE, dO);
+            {
+                uint32_t cq[4][4], dq[4][3];
+                for (int q = 0; q < 4; q++)
+                    for (int b = 0; b < 4; b++) cq[q][b] = (q & 1) ? cO[q >> 1][b] : cE[q >> 1][b];
+                quad_step(sq, cq, dq);
+                for (int q = 0; q < 4; q++)
+                    for (int p = 0; p < 32; p++) {
+                        const int d = dof(q >> 1, q & 1, p);
+                        CHECK(bits_at<3>(dq[q], p) == delta[d], "quad delta line %d step %d d %d", line, i, d);
+                    }
+            }
             for (int h = 0; h < 2; h++)
                 for (int p = 0; p < 32; p++) {
                     CHECK(bits_at<3>(dE[h], p) == delta[dof(h, 0, p)], "delta line %d step %d d %d", line, i, dof(h, 0, p));
@@ -219,6 +268,8 @@ static void check_recurrence(std::mt19937& rng)
                 for (int p = 0; p < 32; p++) {
                     CHECK(bits_at<3>(ln[h].sE, p) == std::min(L[dof(h, 0, p)] - minL, P2), "state");
                     CHECK(bits_at<3>(ln[h].sO, p) == std::min(L[dof(h, 1, p)] - minL, P2), "state");
+                    for (int e = 0; e < 2; e++)
+                        CHECK(bits_at<3>(sq[2 * h + e], p) == std::min(L[dof(h, e, p)] - minL, P2), "quad state");
                 }
         }
     }
@@ -262,12 +313,40 @@ static void check_transpose(std::mt19937& rng)
     }
 }
 
+// The grouped plane layouts: the cost kernel's store word for transpose lane
+// p of the wave's four columns (mvsv_sgbm.hip) is cq_word's (column c, q =
+// 2 h + e) word + bit b, and both layouts tile a row of groups exactly.
+static void check_layouts()
+{
+    for (int p = 0; p < 64; p++) {
+        const int q = p & 31, kq = q >> 3;
+        const int c = ((kq & 1) << 1) | (kq >> 1);
+        const int h = p >> 5, e = (q & 7) >> 2, b = q & 3;
+        const int qw = (2 * (p >> 5) + ((q & 7) >> 2)) * 16 + c * 4 + (q & 3);
+        CHECK((size_t)qw == cq_word(0, c, 2 * h + e) + b, "cost kernel C' word p %d", p);
+    }
+    for (int W1 : {1, 5, 8, 131, 1151}) {
+        const int Wq = padq(W1);
+        std::vector<int> seen16((size_t)Wq * 16, 0), seen12((size_t)Wq * 12, 0);
+        for (int x = 0; x < Wq; x++)
+            for (int q = 0; q < 4; q++) {
+                for (int b = 0; b < 4; b++) seen16[cq_word(0, x, q) + b]++;
+                for (int b = 0; b < 3; b++) seen12[dl_word(0, x, q) + b]++;
+            }
+        for (int v : seen16) CHECK(v == 1, "cq_word tiling W1 %d", W1);
+        for (int v : seen12) CHECK(v == 1, "dl_word tiling W1 %d", W1);
+        CHECK(cq_word((size_t)Wq, 0, 0) == (size_t)Wq * 16, "cq_word row stride");
+        CHECK(dl_word((size_t)Wq, 0, 0) == (size_t)Wq * 12, "dl_word row stride");
+    }
+}
+
 int main()
 {
     std::mt19937 rng(12345);
     check_helpers(rng);
     check_recurrence(rng);
     check_transpose(rng);
+    check_layouts();
     std::printf("bitslice checks: %d failures\n", fails);
     return fails ? 1 : 0;
 }

@@ -1,8 +1,9 @@
 """Host check of the bit-sliced SGM arithmetic (round 5): tests/cpp/bitslice_check.cpp
 runs mvsv_bitslice.hpp's helpers against their scalar definitions, whole scanlines
-of the lane-pair direction step the bit-sliced kernels run (mvsv_bsgm.hip) against
-OpenCV 3.4's recurrence on unclamped costs, and the cost
-kernel's 32 x 32 lane transpose against its definition."""
+of the lane-pair and lane-quad direction steps the bit-sliced kernels run
+(mvsv_bsgm.hip) against OpenCV 3.4's recurrence on unclamped costs (SURVEY
+Appendix A.4), the grouped plane layouts, and the cost kernel's 32 x 32 lane
+transpose against its definition."""
 import os
 import subprocess
 
