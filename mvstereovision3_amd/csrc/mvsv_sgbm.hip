@@ -434,7 +434,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                                                                    int16_t* __restrict__ C,
                                                                    uint8_t* __restrict__ Rv,
                                                                    uint16_t* __restrict__ Mv,
-                                                                   uint32_t* __restrict__ Bv)
+                                                                   uint32_t* __restrict__ Bv, int xcd_bands)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int SH2 = NR / 2;
@@ -446,8 +446,24 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
     // immediate offset from one base per operand
     const int PP = PPC > 0 ? PPC : lay.PP, CL = PPC > 0 ? kCost2Threads / PPC : lay.CL;
     const int TX = CL * kCost2Run, NX = lay.NX;
-    const int f = blockIdx.z;
-    const Cost2Tile tile = cost2_tile(TX, TY, SW2, blockIdx.x, blockIdx.y, W1, H, e.minX1, e.minD, D);
+    // XCD-aware tiles: workgroups go to the 8 XCDs round-robin by linear id
+    // (tools/ubench/xcc_map.hip), so a row band's tiles -- which stage the same
+    // input rows -- land on every XCD and each XCD's L2 fetches the band again.
+    // When the bands divide evenly, XCD x runs whole bands x, x + 8, ... in
+    // order instead (a bijection of the grid: linear id = 8 l + x).
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    {
+        const int GX = gridDim.x, NB = gridDim.y * gridDim.z;
+        if ((NB & 7) == 0 && xcd_bands) {
+            const int id = bx + GX * (by + gridDim.y * bz);
+            const int l = id >> 3, band = (l / GX) * 8 + (id & 7);
+            bx = l % GX;
+            by = band % gridDim.y;
+            bz = band / gridDim.y;
+        }
+    }
+    const int f = bz;
+    const Cost2Tile tile = cost2_tile(TX, TY, SW2, bx, by, W1, H, e.minX1, e.minD, D);
     const int x0 = tile.x0, y0 = tile.y0, y1 = tile.y1, xclo = tile.xclo;
     const int nL = tile.nL;
     const size_t plane = (size_t)W * H;
@@ -3186,7 +3202,7 @@ int launch_paths_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
 
 }  // namespace
 
-using Cost2Kern = void (*)(const uint64_t*, int, int, SgbmEff, int, int16_t*, uint8_t*, uint16_t*, uint32_t*);
+using Cost2Kern = void (*)(const uint64_t*, int, int, SgbmEff, int, int16_t*, uint8_t*, uint16_t*, uint32_t*, int);
 template <int STG, int PPC>
 static Cost2Kern cost2_pick_nr(int nr)
 {
@@ -3243,7 +3259,7 @@ static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int
             {
                 StageTimer tm(ctx, kStageCost);
                 hipLaunchKernelGGL(kern, grid2, dim3(kCost2Threads), l2.bytes, s, pre, W, H, e, TY,
-                                   Cv, *Bv ? nullptr : *Rv, Mv, *Bv);
+                                   Cv, *Bv ? nullptr : *Rv, Mv, *Bv, ctx->cost_xcd ? 1 : 0);
             }
             *pinned_hh = e.fullDP != 0;  // MODE_HH fix-up rows/column written by the kernel
             return check_hip(ctx, hipGetLastError(), "sgbm cost kernel");

@@ -338,6 +338,10 @@ static void copy_options(mvsv_ctx* d, const mvsv_ctx* s)
     d->strip_tickets = s->strip_tickets;
     d->bm2 = s->bm2;
     d->bm_ty = s->bm_ty;
+    d->bitslice = s->bitslice;
+    d->bs_groups = s->bs_groups;
+    d->bs_serial = s->bs_serial;
+    d->cost_xcd = s->cost_xcd;
 }
 
 int mvsv_stream_set_inflight(mvsv_stream* st, int n)
