@@ -156,6 +156,21 @@ MVSV_BS_HD void add54(const uint32_t (&a)[5], const uint32_t (&b)[4], uint32_t (
     v[5] = a[4] & k3;
 }
 
+// v = a + b, both 5-bit, the sum known to be < 64 (6-bit result, 10 instructions)
+MVSV_BS_HD void add55(const uint32_t (&a)[5], const uint32_t (&b)[5], uint32_t (&v)[6])
+{
+    const uint32_t k0 = a[0] & b[0];
+    v[0] = a[0] ^ b[0];
+    v[1] = lop3<kXor3>(a[1], b[1], k0);
+    const uint32_t k1 = lop3<kMaj>(a[1], b[1], k0);
+    v[2] = lop3<kXor3>(a[2], b[2], k1);
+    const uint32_t k2 = lop3<kMaj>(a[2], b[2], k1);
+    v[3] = lop3<kXor3>(a[3], b[3], k2);
+    const uint32_t k3 = lop3<kMaj>(a[3], b[3], k2);
+    v[4] = lop3<kXor3>(a[4], b[4], k3);
+    v[5] = lop3<kMaj>(a[4], b[4], k3);
+}
+
 // s = min(v - m, P2) for a 4-bit v >= m and a lane-uniform 3-bit m given as
 // all-ones / all-zero masks m0..m2 (13 instructions)
 template <int P2>

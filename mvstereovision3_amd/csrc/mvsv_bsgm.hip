@@ -558,6 +558,102 @@ __global__ __launch_bounds__(64) void bsgm_lines4_kernel(const uint32_t* __restr
 }
 
 // ---------------------------------------------------------------------------
+// Side by side (launches too small to fill the GPU with strip chains -- one or
+// two camera frames, path_schedule 2): every direction on its own lane-quad
+// chains, no strip hand-offs and no block barriers.  The vertical / diagonal
+// directions step row by row (t; y = t down, H - 1 - t up), 16 chains per wave
+// (lane 4 c + q: chain k0 + c, words (h, e) = (q >> 1, q & 1)), chain k on
+// cell x = k + DX t; a chain outside the image carries the zero state (a path
+// starts at the border).  Each direction writes its own grouped delta plane.
+// A chain is as long as the image is tall, so a step costs the lane-quad
+// step's latency (tools/ubench/bs_chain: 348 cycles) instead of a strip
+// block's barrier-synchronised step.
+// ---------------------------------------------------------------------------
+constexpr int kBsDPF = 16;  // steps of C' prefetch
+
+template <int DX, int P1, int P2>
+__device__ __forceinline__ void bs_dir_chains(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dp,
+                                              size_t plane_words, int H, int W1, uint32_t* __restrict__ dummy,
+                                              int pass)
+{
+    const int lane = threadIdx.x;
+    const int c = lane >> 2, q = lane & 3;
+    const int f = blockIdx.y;
+    const bool odd = (q & 1) != 0;
+    const uint32_t fill_hi = q == 3 ? kOnes : 0u, fill_lo = q == 0 ? kOnes : 0u, sh = odd ? 1u : 31u;
+    const int kmin = DX > 0 ? -(H - 1) : 0;
+    const int kend = DX < 0 ? W1 + H - 1 : W1;
+    const int k0 = kmin + (int)blockIdx.x * 16;
+    if (k0 >= kend) return;
+    const int k = k0 + c;
+    // the wave's steps with some cell inside the image
+    const int tb = DX > 0 ? max(0, -(k0 + 15)) : DX < 0 ? max(0, k0 - W1 + 1) : 0;
+    const int te = DX > 0 ? min(H, W1 - k0) : DX < 0 ? min(H, k0 + 16) : H;
+    if (tb >= te) return;
+    const int W1q = bs::padq(W1);
+    const size_t fb = (size_t)f * H;
+    uint32_t* dplane = Dp + (size_t)(pass * 3 + (1 - DX)) * plane_words;  // slot: DX +1, 0, -1
+    auto cell = [&](int t, int& x, size_t& rowq) {
+        x = k + DX * t;
+        rowq = (fb + (pass == 0 ? t : H - 1 - t)) * W1q;
+        return k < kend && x >= 0 && x < W1;
+    };
+    auto coff = [&](int t) -> size_t {
+        int x;
+        size_t rowq;
+        return cell(t, x, rowq) ? bs::cq_word(rowq, x, q) : bs::cq_word(fb * W1q, 0, q);
+    };
+    uint4 cr[kBsDPF];
+#pragma unroll
+    for (int j = 0; j < kBsDPF; j++) {
+        cr[j] = *(const uint4*)(Bc + coff(min(tb + j, te - 1)));
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t st[3] = {0u, 0u, 0u};
+    auto step = [&](int t, int j) {
+        int x;
+        size_t rowq;
+        const bool valid = cell(t, x, rowq);
+        const uint32_t cw[4] = {cr[j].x, cr[j].y, cr[j].z, cr[j].w};
+        uint32_t nw[3], dw[3];
+        bs_quad_step<P1, P2>(st, cw, fill_hi, fill_lo, odd, sh, nw, dw);
+        cr[j] = *(const uint4*)(Bc + coff(min(t + kBsDPF, te - 1)));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int b = 0; b < 3; b++) st[b] = valid ? nw[b] : 0u;
+        // unpredicated: a cell outside the image stores into the lane's dummy slot
+        uint32_t* o = valid ? dplane + bs::dl_word(rowq, x, q) : dummy + lane * 4;
+        o[0] = dw[0];
+        o[1] = dw[1];
+        o[2] = dw[2];
+    };
+    int t = tb;
+    for (; t + kBsDPF <= te; t += kBsDPF) {
+#pragma unroll
+        for (int j = 0; j < kBsDPF; j++) step(t + j, j);
+    }
+#pragma unroll
+    for (int j = 0; j < kBsDPF; j++)
+        if (t + j < te) step(t + j, j);
+}
+
+// blockIdx.z = pass * 3 + slot (slot 0, 1, 2: DX = +1, 0, -1); blockIdx.x: 16
+// chains, as many as the longest direction has (W1 + H - 1)
+template <int P1, int P2>
+__global__ __launch_bounds__(64) void bsgm_dir_kernel(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dp,
+                                                       size_t plane_words, int H, int W1,
+                                                       uint32_t* __restrict__ dummy)
+{
+    const int pass = blockIdx.z / 3, slot = blockIdx.z - 3 * pass;
+    if (slot == 0)
+        bs_dir_chains<1, P1, P2>(Bc, Dp, plane_words, H, W1, dummy, pass);
+    else if (slot == 1)
+        bs_dir_chains<0, P1, P2>(Bc, Dp, plane_words, H, W1, dummy, pass);
+    else
+        bs_dir_chains<-1, P1, P2>(Bc, Dp, plane_words, H, W1, dummy, pass);
+}
+
+// ---------------------------------------------------------------------------
 // WTA: one block per image row.  S'' = 8 C' + A_down + A_up + d_LR + d_RL (7
 // bits; DESIGN.md §4b: same argmin and ties as S, exact minimum n (m - P2) +
 // min S''), argmin with the smallest d on ties (MODE_HH), S''(best -+ 1) read
@@ -567,6 +663,7 @@ __global__ __launch_bounds__(64) void bsgm_lines4_kernel(const uint32_t* __restr
 // ---------------------------------------------------------------------------
 constexpr int kBsWtaThreads = 512;
 
+template <bool SIDE>
 __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t* __restrict__ Bc,
                                                                  const uint32_t* __restrict__ A, size_t aplane,
                                                                  const uint32_t* __restrict__ Dl, size_t dplane,
@@ -596,7 +693,35 @@ __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t*
         const int x = min(xr, W1 - 1);
         const size_t pix = pix0 + x;
         uint32_t c[2][4], ad[2][4], au[2][4], dl[2][3], dr[2][3];
-        {
+        uint32_t S[2][7];
+        if constexpr (SIDE) {
+            // eight grouped delta planes (six side-by-side directions, then the
+            // two line directions): S'' = 8 C' + the eight deltas
+            const size_t rowq = (size_t)(f * H + y) * bs::padq(W1);
+            const uint32_t* qc = Bc + bs::cq_word(rowq, x, 2 * h);
+#pragma unroll
+            for (int e2 = 0; e2 < 2; e2++) {
+                const uint4 t = *(const uint4*)(qc + 16 * e2);
+                c[e2][0] = t.x, c[e2][1] = t.y, c[e2][2] = t.z, c[e2][3] = t.w;
+                uint32_t dd[8][3];
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const uint32_t* qd = Dl + (size_t)i * dplane + bs::dl_word(rowq, x, 2 * h + e2);
+#pragma unroll
+                    for (int b = 0; b < 3; b++) dd[i][b] = qd[b];
+                }
+                uint32_t a4[4][4], a5[2][5], s6[6], hi[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) bs::add33(dd[2 * i], dd[2 * i + 1], a4[i]);
+                bs::add44(a4[0], a4[1], a5[0]);
+                bs::add44(a4[2], a4[3], a5[1]);
+                bs::add55(a5[0], a5[1], s6);  // all deltas <= 8 P2 = 40
+                const uint32_t top[3] = {s6[3], s6[4], s6[5]};
+                bs::add43(c[e2], top, hi);
+                S[e2][0] = s6[0], S[e2][1] = s6[1], S[e2][2] = s6[2];
+                S[e2][3] = hi[0], S[e2][4] = hi[1], S[e2][5] = hi[2], S[e2][6] = hi[3];
+            }
+        } else {
             // grouped C' and line planes (bs::cq_word / dl_word), E then O
             const size_t rowq = (size_t)(f * H + y) * bs::padq(W1);
             const uint32_t* qc = Bc + bs::cq_word(rowq, x, 2 * h);
@@ -619,18 +744,17 @@ __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t*
                     dr[e2][b] = qr[12 * e2 + b];
                 }
             }
-        }
-        uint32_t S[2][7];
 #pragma unroll
-        for (int e2 = 0; e2 < 2; e2++) {
-            uint32_t s5[5], d4[4], s6[6], hi[4];
-            bs::add44(ad[e2], au[e2], s5);  // strips <= 2 * 3 P2 = 30
-            bs::add33(dl[e2], dr[e2], d4);  // lines <= 2 P2 = 10
-            bs::add54(s5, d4, s6);          // all deltas <= 8 P2 = 40
-            const uint32_t top[3] = {s6[3], s6[4], s6[5]};
-            bs::add43(c[e2], top, hi);      // 8 C' + deltas: high part <= 10 + 5
-            S[e2][0] = s6[0], S[e2][1] = s6[1], S[e2][2] = s6[2];
-            S[e2][3] = hi[0], S[e2][4] = hi[1], S[e2][5] = hi[2], S[e2][6] = hi[3];
+            for (int e2 = 0; e2 < 2; e2++) {
+                uint32_t s5[5], d4[4], s6[6], hi[4];
+                bs::add44(ad[e2], au[e2], s5);  // strips <= 2 * 3 P2 = 30
+                bs::add33(dl[e2], dr[e2], d4);  // lines <= 2 P2 = 10
+                bs::add54(s5, d4, s6);          // all deltas <= 8 P2 = 40
+                const uint32_t top[3] = {s6[3], s6[4], s6[5]};
+                bs::add43(c[e2], top, hi);      // 8 C' + deltas: high part <= 10 + 5
+                S[e2][0] = s6[0], S[e2][1] = s6[1], S[e2][2] = s6[2];
+                S[e2][3] = hi[0], S[e2][4] = hi[1], S[e2][5] = hi[2], S[e2][6] = hi[3];
+            }
         }
         // argmin: the minimum is <= 8 P2 = 40 < 64 (the d with C' = 0), so bit 6 is 0
         uint32_t kE = ~S[0][6], kO = ~S[1][6];
@@ -806,10 +930,57 @@ static int launch_bs_strips(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const
     return rc;
 }
 
-int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv, const uint32_t* Bv,
-               const uint16_t* Mv, int16_t* raw)
+// Small launches (path_schedule 2): the six vertical / diagonal directions as
+// independent lane-quad chains (one launch) beside the two line directions (aux
+// stream), eight delta planes, then the WTA over all eight.
+static int bsgm_paths_side(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv,
+                           const uint32_t* Bv, const uint16_t* Mv, int16_t* raw)
 {
     int rc;
+    const size_t dplane = (size_t)n * H * bs::padq(e.W1) * 12;  // words per delta plane (grouped)
+    // + 256 words: dummy store slots of cells outside the image
+    if ((rc = ensure(ctx, ctx->agg, (8 * dplane + 256) * 4, "bit-sliced delta planes"))) return rc;
+    if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
+    uint32_t* Dv = (uint32_t*)ctx->agg.ptr;
+    hipStream_t s = ctx->stream;
+    if (!ctx->aux) {
+        if ((rc = check_hip(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking), "aux stream")) ||
+            (rc = check_hip(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming), "event")) ||
+            (rc = check_hip(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming), "event")))
+            return rc;
+    }
+    {
+        StageTimer tm(ctx, kStagePath);
+        if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_fork, s), "fork")) ||
+            (rc = check_hip(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0), "fork wait")))
+            return rc;
+        {
+            StageTimer tl(ctx, kStageLines, ctx->aux);
+            hipLaunchKernelGGL((bsgm_lines4_kernel<2, 5>), dim3((H + 15) / 16, n, 2), dim3(64), 0, ctx->aux, Bv,
+                               Dv + 6 * dplane, dplane, H, e.W1, 0);
+            if ((rc = check_hip(ctx, hipGetLastError(), "bit-sliced line kernel"))) return rc;
+        }
+        {
+            StageTimer ts(ctx, kStageStrips);
+            hipLaunchKernelGGL((bsgm_dir_kernel<2, 5>), dim3((e.W1 + H - 1 + 15) / 16, n, 6), dim3(64), 0, s, Bv,
+                               Dv, dplane, H, e.W1, Dv + 8 * dplane);
+            if ((rc = check_hip(ctx, hipGetLastError(), "bit-sliced direction kernel"))) return rc;
+        }
+        if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_join, ctx->aux), "join")) ||
+            (rc = check_hip(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0), "join wait")))
+            return rc;
+    }
+    StageTimer tm(ctx, kStageFinal);
+    hipLaunchKernelGGL(bsgm_wta_kernel<true>, dim3(H, n), dim3(kBsWtaThreads), 0, s, Bv, nullptr, (size_t)0, Dv,
+                       dplane, Cv, Mv, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
+    return check_hip(ctx, hipGetLastError(), "bit-sliced WTA kernel");
+}
+
+int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv, const uint32_t* Bv,
+               const uint16_t* Mv, int16_t* raw, bool side)
+{
+    int rc;
+    if (side) return bsgm_paths_side(ctx, n, H, W, e, Cv, Bv, Mv, raw);
     const size_t aplane = (size_t)n * H * e.W1 * 16;  // words per strip-pass plane
     const size_t dplane = (size_t)n * H * bs::padq(e.W1) * 12;  // words per line plane (grouped, padded rows)
     // + 512 words: the strip kernel's dummy store slots (cells outside the image)
@@ -860,7 +1031,7 @@ int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16
             return rc;
     }
     StageTimer tm(ctx, kStageFinal);
-    hipLaunchKernelGGL(bsgm_wta_kernel, dim3(H, n), dim3(kBsWtaThreads), 0, s, Bv, Av, aplane, Dv, dplane, Cv, Mv, H,
+    hipLaunchKernelGGL(bsgm_wta_kernel<false>, dim3(H, n), dim3(kBsWtaThreads), 0, s, Bv, Av, aplane, Dv, dplane, Cv, Mv, H,
                        W, e, raw, (uint32_t*)ctx->keys.ptr);
     return check_hip(ctx, hipGetLastError(), "bit-sliced WTA kernel");
 }

@@ -200,7 +200,7 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
 bool bsgm_eligible(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H);
 size_t bsgm_plane_bytes(int n, int H, int W1);
 int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv, const uint32_t* Bv,
-               const uint16_t* Mv, int16_t* raw);
+               const uint16_t* Mv, int16_t* raw, bool side);
 int median3x3_device(mvsv_ctx* ctx, int n, const int16_t* src, size_t ss, size_t sfs,
                      int16_t* dst, size_t ds, size_t dfs, int W, int H,
                      const int* poison = nullptr, unsigned epoch = 0, int invalid = 0);

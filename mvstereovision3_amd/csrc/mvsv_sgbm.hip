@@ -3308,11 +3308,11 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     // direction passes are sized by bsgm_paths
     // accumulator planes: one per concurrently written direction group
     const int sched = path_schedule(ctx, e, H, n);
-    // (launches too small to fill the GPU with strips -- one camera frame --
-    // keep the directions side by side: the bit-sliced passes trade fewer
-    // instructions for a longer serial chain per scanline)
-    const bool bs = bsgm_eligible(ctx, e, n, H) && sched == 1 && ctx->path16 && ctx->tri && ctx->cost2 &&
-                    ctx->cost_fixed_pp && e.SH2 <= 7 && e.SW2 == e.SH2;
+    // (frame batches: the bit-sliced strips; launches too small to fill the
+    // GPU with strips -- one camera frame, schedule 2 -- the bit-sliced
+    // directions side by side, each on its own chains: bsgm_paths)
+    const bool bs = bsgm_eligible(ctx, e, n, H) && (sched == 1 || sched == 2) && ctx->path16 && ctx->tri &&
+                    ctx->cost2 && ctx->cost_fixed_pp && e.SH2 <= 7 && e.SW2 == e.SH2;
     uint32_t* Bv = nullptr;
     const int nplanes = sched == 2 ? (e.fullDP ? 7 : 4) : sched == 1 ? (e.fullDP ? 3 : 2) : 1;
     // 4-bit planes: one per direction (side by side, P2 <= 15) or per strip
@@ -3414,7 +3414,7 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     const int np = (e.D + 127) / 128;
     const bool wide = ctx->path16 && (e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256);
     if (Bv) {
-        rc = bsgm_paths(ctx, n, H, W, e, Cv, Bv, Mv, raw);
+        rc = bsgm_paths(ctx, n, H, W, e, Cv, Bv, Mv, raw, sched == 2);
     } else if (wide) {
         switch (e.D) {
         case 32: rc = launch_paths16_acc<1>(ctx, n, H, W, e, Cv, Rv, Mv, Sv, raw); break;

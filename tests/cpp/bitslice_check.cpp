@@ -67,6 +67,8 @@ static void check_helpers(std::mt19937& rng)
         uint32_t sm[3] = {s[0], s[1], s[2]};
         add43(c4, sm, v);
         add54(a5, a4, w6);
+        uint32_t w6b[6];
+        add55(a5, a5, w6b);
         for (int p = 0; p < 32; p++) {
             CHECK(bits_at<3>(r, p) == std::min(va[p], vb[p]), "min3b");
             CHECK(bits_at<3>(u, p) == std::min(va[p] + P1, P2), "gmap");
@@ -76,6 +78,7 @@ static void check_helpers(std::mt19937& rng)
             CHECK(bits_at<5>(w5, p) == 2 * v4[p], "add44");
             CHECK(bits_at<4>(v, p) == vc[p] + vs[p], "add43");
             CHECK(bits_at<6>(w6, p) == v5[p] + v4[p], "add54");
+            CHECK(bits_at<6>(w6b, p) == 2 * v5[p], "add55");
         }
         // subclamp: v >= m, m lane-uniform in [0, P2]
         const int m = rng() % (P2 + 1);

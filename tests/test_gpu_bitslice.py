@@ -2,8 +2,9 @@
 (MODE_HH, numDisparities 128, P1 2 / P2 5 -- configs/sgbm.yml's effective penalties
 --, uniquenessRatio 0, no int16 wrap) the six strip directions, the two row
 directions and the WTA run on bit planes.  Every case runs with the bit-sliced
-path (the default) and forced off (MVSV_OPT_BITSLICE = 0, the packed int16
-kernels), and both must be bit-exact against the oracle.
+path on strips (frame batches), side by side (small launches) and forced off
+(MVSV_OPT_BITSLICE = 0, the packed int16 kernels), and all must be bit-exact
+against the oracle.
 Reference: Disparity::sgbm (src/disparity.cpp:6-10) -> cv::StereoSGBM::compute;
 mode from loadSGBMParameters (src/disparity.cpp:92-95)."""
 import numpy as np
@@ -26,9 +27,11 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("bits", [1, 0])
+# (bit-sliced, path schedule): strips (1), side by side (2: each direction on its
+# own chains, the small-launch form), the packed int16 kernels on strips
+@pytest.mark.parametrize("bits,sched", [(1, 1), (1, 2), (0, 1)])
 @pytest.mark.parametrize("case", range(len(CASES)))
-def test_bitslice_hh_forced(gpu, mvsv, oracle, case, bits):
+def test_bitslice_hh_forced(gpu, mvsv, oracle, case, bits, sched):
     from mvstereovision3_amd import _lib
     H, W, bs, P1, P2, minD, d12 = CASES[case]
     rng = np.random.default_rng(5100 + 7 * case)
@@ -38,15 +41,13 @@ def test_bitslice_hh_forced(gpu, mvsv, oracle, case, bits):
               uniquenessRatio=0, speckleWindowSize=int(rng.choice([0, 20])), speckleRange=2, mode=1)
     variant = int(rng.integers(0, 4))
     try:
-        # single frames run the directions side by side unless the strip
-        # schedule is forced -- the schedule the bit-sliced path replaces
-        _lib.set_option(_lib.OPT_PATH_SCHEDULE, 1)
+        _lib.set_option(_lib.OPT_PATH_SCHEDULE, sched)
         _lib.set_option(_lib.OPT_BITSLICE, bits)
         got, want = sgbm_both(mvsv, oracle, L, R, variant=variant, **kw)
     finally:
         _lib.set_option(_lib.OPT_BITSLICE, 1)
         _lib.set_option(_lib.OPT_PATH_SCHEDULE, 0)
-    assert np.array_equal(got, want), f"bitslice={bits} variant={variant} {kw}: " + report(got, want)
+    assert np.array_equal(got, want), f"bitslice={bits} sched={sched} variant={variant} {kw}: " + report(got, want)
 
 
 @pytest.mark.parametrize("groups", ["1", "2", "4", "5", "2-side"])
