@@ -590,18 +590,20 @@ __device__ __forceinline__ void bs_dir_chains(const uint32_t* __restrict__ Bc, u
     const int tb = DX > 0 ? max(0, -(k0 + 15)) : DX < 0 ? max(0, k0 - W1 + 1) : 0;
     const int te = DX > 0 ? min(H, W1 - k0) : DX < 0 ? min(H, k0 + 16) : H;
     if (tb >= te) return;
+    // 32-bit word offsets (bsgm_eligible bounds a plane below 2^31 words),
+    // branch-free: the cell's column clamped into the row for the loads, the
+    // validity only selects the state reset and the store slot
     const int W1q = bs::padq(W1);
-    const size_t fb = (size_t)f * H;
+    const int row0 = f * H + (pass == 0 ? 0 : H - 1), rs = pass == 0 ? 1 : -1;
     uint32_t* dplane = Dp + (size_t)(pass * 3 + (1 - DX)) * plane_words;  // slot: DX +1, 0, -1
-    auto cell = [&](int t, int& x, size_t& rowq) {
-        x = k + DX * t;
-        rowq = (fb + (pass == 0 ? t : H - 1 - t)) * W1q;
-        return k < kend && x >= 0 && x < W1;
+    auto xrow = [&](int t, int& xc) -> uint32_t {
+        xc = min(max(k + DX * t, 0), W1 - 1);
+        return (uint32_t)(row0 + rs * t) * (uint32_t)W1q + (uint32_t)(xc & ~3);
     };
-    auto coff = [&](int t) -> size_t {
-        int x;
-        size_t rowq;
-        return cell(t, x, rowq) ? bs::cq_word(rowq, x, q) : bs::cq_word(fb * W1q, 0, q);
+    auto coff = [&](int t) -> uint32_t {
+        int xc;
+        const uint32_t g = xrow(t, xc);
+        return g * 16u + (uint32_t)(q * 16 + (xc & 3) * 4);
     };
     uint4 cr[kBsDPF];
 #pragma unroll
@@ -611,9 +613,7 @@ __device__ __forceinline__ void bs_dir_chains(const uint32_t* __restrict__ Bc, u
     }
     uint32_t st[3] = {0u, 0u, 0u};
     auto step = [&](int t, int j) {
-        int x;
-        size_t rowq;
-        const bool valid = cell(t, x, rowq);
+        const bool valid = k < kend && (unsigned)(k + DX * t) < (unsigned)W1;
         const uint32_t cw[4] = {cr[j].x, cr[j].y, cr[j].z, cr[j].w};
         uint32_t nw[3], dw[3];
         bs_quad_step<P1, P2>(st, cw, fill_hi, fill_lo, odd, sh, nw, dw);
@@ -622,7 +622,9 @@ __device__ __forceinline__ void bs_dir_chains(const uint32_t* __restrict__ Bc, u
 #pragma unroll
         for (int b = 0; b < 3; b++) st[b] = valid ? nw[b] : 0u;
         // unpredicated: a cell outside the image stores into the lane's dummy slot
-        uint32_t* o = valid ? dplane + bs::dl_word(rowq, x, q) : dummy + lane * 4;
+        int xc;
+        const uint32_t g = xrow(t, xc);
+        uint32_t* o = valid ? dplane + (g * 12u + (uint32_t)(q * 12 + (xc & 3) * 3)) : dummy + lane * 4;
         o[0] = dw[0];
         o[1] = dw[1];
         o[2] = dw[2];
@@ -850,7 +852,7 @@ bool bsgm_eligible(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H)
     const long bs = 2L * e.SW2 + 1;
     const bool no_wrap = (long)e.P2 + bs * bs * (2L * e.ftzero + 63) + e.P2 <= 32767;
     return ctx->bitslice && e.fullDP && e.D == 128 && e.P1 == 2 && e.P2 == 5 && e.uniq == 0 && no_wrap &&
-           e.W1 > 0 && (size_t)n * H * e.W1 * 16 < ((size_t)1 << 31);
+           e.W1 > 0 && (size_t)n * H * bs::padq(e.W1) * 16 < ((size_t)1 << 31);
 }
 
 size_t bsgm_plane_bytes(int n, int H, int W1) { return (size_t)n * H * bs::padq(W1) * 64; }
