@@ -459,8 +459,8 @@ __global__ __launch_bounds__(BsStripCfg<NG>::kThreads) void bsgm_strip_kernel(
 constexpr int kBsLG = 8;
 
 template <int P1, int P2>
-__global__ __launch_bounds__(64) void bsgm_lines4_kernel(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dl,
-                                                          size_t plane_words, int H, int W1, int probe)
+__device__ __forceinline__ void bs_line_chains(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dl,
+                                               size_t plane_words, int H, int W1, int probe, bool rl)
 {
     const int lane = threadIdx.x;
     const int q = lane & 3, rr = lane >> 2;
@@ -551,10 +551,17 @@ __global__ __launch_bounds__(64) void bsgm_lines4_kernel(const uint32_t* __restr
                 ring(i + j, j, part);
         }
     };
-    if (blockIdx.z != 0)
+    if (rl)
         run(std::true_type());
     else
         run(std::false_type());
+}
+
+template <int P1, int P2>
+__global__ __launch_bounds__(64) void bsgm_lines4_kernel(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dl,
+                                                          size_t plane_words, int H, int W1, int probe)
+{
+    bs_line_chains<P1, P2>(Bc, Dl, plane_words, H, W1, probe, blockIdx.z != 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -640,12 +647,19 @@ __device__ __forceinline__ void bs_dir_chains(const uint32_t* __restrict__ Bc, u
 }
 
 // blockIdx.z = pass * 3 + slot (slot 0, 1, 2: DX = +1, 0, -1); blockIdx.x: 16
-// chains, as many as the longest direction has (W1 + H - 1)
+// chains, as many as the longest direction has (W1 + H - 1).  z = 6, 7: the two
+// line directions (16 rows per block) into planes 6 and 7 -- one launch for all
+// eight directions (a small launch pays no stream fork / join)
 template <int P1, int P2>
 __global__ __launch_bounds__(64) void bsgm_dir_kernel(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dp,
                                                        size_t plane_words, int H, int W1,
                                                        uint32_t* __restrict__ dummy)
 {
+    if (blockIdx.z >= 6) {
+        if ((int)blockIdx.x * 16 < H)
+            bs_line_chains<P1, P2>(Bc, Dp + 6 * plane_words, plane_words, H, W1, 0, blockIdx.z == 7);
+        return;
+    }
     const int pass = blockIdx.z / 3, slot = blockIdx.z - 3 * pass;
     if (slot == 0)
         bs_dir_chains<1, P1, P2>(Bc, Dp, plane_words, H, W1, dummy, pass);
@@ -932,9 +946,8 @@ static int launch_bs_strips(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const
     return rc;
 }
 
-// Small launches (path_schedule 2): the six vertical / diagonal directions as
-// independent lane-quad chains (one launch) beside the two line directions (aux
-// stream), eight delta planes, then the WTA over all eight.
+// Small launches (path_schedule 2): all eight directions as independent
+// lane-quad chains in one launch, eight delta planes, then the WTA over them.
 static int bsgm_paths_side(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv,
                            const uint32_t* Bv, const uint16_t* Mv, int16_t* raw)
 {
@@ -945,32 +958,11 @@ static int bsgm_paths_side(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e,
     if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
     uint32_t* Dv = (uint32_t*)ctx->agg.ptr;
     hipStream_t s = ctx->stream;
-    if (!ctx->aux) {
-        if ((rc = check_hip(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking), "aux stream")) ||
-            (rc = check_hip(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming), "event")) ||
-            (rc = check_hip(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming), "event")))
-            return rc;
-    }
     {
         StageTimer tm(ctx, kStagePath);
-        if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_fork, s), "fork")) ||
-            (rc = check_hip(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0), "fork wait")))
-            return rc;
-        {
-            StageTimer tl(ctx, kStageLines, ctx->aux);
-            hipLaunchKernelGGL((bsgm_lines4_kernel<2, 5>), dim3((H + 15) / 16, n, 2), dim3(64), 0, ctx->aux, Bv,
-                               Dv + 6 * dplane, dplane, H, e.W1, 0);
-            if ((rc = check_hip(ctx, hipGetLastError(), "bit-sliced line kernel"))) return rc;
-        }
-        {
-            StageTimer ts(ctx, kStageStrips);
-            hipLaunchKernelGGL((bsgm_dir_kernel<2, 5>), dim3((e.W1 + H - 1 + 15) / 16, n, 6), dim3(64), 0, s, Bv,
-                               Dv, dplane, H, e.W1, Dv + 8 * dplane);
-            if ((rc = check_hip(ctx, hipGetLastError(), "bit-sliced direction kernel"))) return rc;
-        }
-        if ((rc = check_hip(ctx, hipEventRecord(ctx->ev_join, ctx->aux), "join")) ||
-            (rc = check_hip(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0), "join wait")))
-            return rc;
+        hipLaunchKernelGGL((bsgm_dir_kernel<2, 5>), dim3((e.W1 + H - 1 + 15) / 16, n, 8), dim3(64), 0, s, Bv, Dv,
+                           dplane, H, e.W1, Dv + 8 * dplane);
+        if ((rc = check_hip(ctx, hipGetLastError(), "bit-sliced direction kernel"))) return rc;
     }
     StageTimer tm(ctx, kStageFinal);
     hipLaunchKernelGGL(bsgm_wta_kernel<true>, dim3(H, n), dim3(kBsWtaThreads), 0, s, Bv, nullptr, (size_t)0, Dv,
