@@ -677,6 +677,67 @@ __global__ __launch_bounds__(64) void bsgm_dir_kernel(const uint32_t* __restrict
 // parabola, right-view keys (order-independent atomicMin), then the row's LR
 // check (the final loop of OpenCV 3.4).
 // ---------------------------------------------------------------------------
+// The WTA's per-pixel tail (both WTA forms and bsgm_rl_final_kernel): exact
+// S(best -+ 1) from S'' and, where the residual may be clamped, the C gathers;
+// the parabola, the raw map, the right-view key.  best / mins / Sm / Sp: argmin,
+// minimum S'' and S''(best -+ 1) of pixel pix (cost column x of its row).
+constexpr int kBsNdir = 8;
+__device__ __forceinline__ void bs_finish_pixel(const int16_t* __restrict__ C, const uint16_t* __restrict__ Mv,
+                                                size_t pix, int W1, int W, int x, int best, int mins, int Sm,
+                                                int Sp, const SgbmEff& e, int16_t* orow, uint32_t* krow)
+{
+    const int D = e.D;
+    const int clampS = kBsNdir * 2 * e.P2;  // S'' >= this: C'' may be the clamp value
+    const int mC = Mv[pix];
+    const int base = kBsNdir * (mC - e.P2);  // S = min(base + S', MAX_COST)
+    const int bm = max(best - 1, 0), bp = min(best + 1, D - 1);
+    const bool need = Sm >= clampS || Sp >= clampS;
+    // C is stored [frame][y][x / 4][d][x % 4] on this pipeline (the cost
+    // kernel's bit-sliced mode, rows padded to 4 pixels)
+    const int prow = (int)(pix / W1), px = (int)(pix - (size_t)prow * W1);
+    const size_t cbase = ((size_t)prow * ((W1 + 3) & ~3) + (px & ~3)) * D + (px & 3);
+    auto cword = [&](int d) -> int { return need ? (int)(uint16_t)C[cbase + d * 4] : 0; };
+    auto exact = [&](int Spp, int cv) -> int {
+        const int c1 = Spp >= clampS ? cv - mC : 0;
+        return min(base + Spp + kBsNdir * (c1 - min(c1, 2 * e.P2)), kMaxCost);
+    };
+    const int minS = min(base + mins, kMaxCost);
+    const int Smx = exact(Sm, cword(bm)), Spx = exact(Sp, cword(bp));
+    int bst = best;
+    if (minS >= kMaxCost) bst = -1;  // no strict minimum below MAX_COST
+    const int den = max(Smx + Spx - 2 * minS, 1);
+    const int frac = ((Smx - Spx) * kDispScale + den) / (den * 2);
+    const int d16 = bst * kDispScale + (frac & -(int)(0 < bst && bst < D - 1));
+    orow[x + e.minX1] = (int16_t)(d16 + e.minD * kDispScale);
+    const int x2 = x + e.minX1 - bst - e.minD;
+    if (minS < kMaxCost && x2 >= 0 && x2 < W)
+        atomicMin(krow + x2, ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
+}
+
+// left-right check of a finished row (OpenCV 3.4 final loop), nthreads threads
+__device__ __forceinline__ void bs_lr_check_row(int16_t* orow, const uint32_t* krow, int W, const SgbmEff& e,
+                                                int nthreads)
+{
+    const int INV = e.invalid, minX1 = e.minX1, minD = e.minD;
+    for (int x = minX1 + threadIdx.x; x < e.maxX1; x += nthreads) {
+        const int v = orow[x];
+        if (v == INV) continue;
+        const int dlo = v >> kDispShift, dhi = (v + kDispScale - 1) >> kDispShift;
+        const int xl = x - dlo, xh = x - dhi;
+        auto d2at = [&](int xx) -> int {
+            const uint32_t kk = __hip_atomic_load(krow + xx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (kk == 0xffffffffu) return INV;
+            const int xc = 0xffff - (int)(kk & 0xffffu);
+            return xc + minX1 - xx;
+        };
+        if (0 <= xl && xl < W && 0 <= xh && xh < W) {
+            const int a = d2at(xl), b = d2at(xh);
+            if (a >= minD && abs(a - dlo) > e.disp12 && b >= minD && abs(b - dhi) > e.disp12)
+                orow[x] = (int16_t)INV;
+        }
+    }
+}
+
 constexpr int kBsWtaThreads = 512;
 
 template <bool SIDE>
@@ -688,9 +749,8 @@ __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t*
                                                                  SgbmEff e, int16_t* __restrict__ raw,
                                                                  uint32_t* __restrict__ keys)
 {
-    constexpr int NDIR = 8;
     const int y = blockIdx.x, f = blockIdx.y;
-    const int D = e.D, W1 = e.W1, minD = e.minD, minX1 = e.minX1;
+    const int W1 = e.W1;
     const int INV = e.invalid;
     int16_t* orow = raw + ((size_t)f * H + y) * W;
     uint32_t* krow = keys + ((size_t)f * H + y) * W;
@@ -702,7 +762,6 @@ __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t*
     __syncthreads();
     const int h = threadIdx.x & 1;
     const size_t pix0 = ((size_t)f * H + y) * W1;
-    const int clampS = NDIR * 2 * e.P2;  // S'' >= this: C'' may be the clamp value
     for (int xb = 0; xb < W1; xb += kBsWtaThreads / 2) {
         const int xr = xb + (threadIdx.x >> 1);
         const bool own = xr < W1;
@@ -807,53 +866,179 @@ __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t*
             if (((best - 1) >> 6) != h) Sm = Smo;
             if (((best + 1) >> 6) != h) Sp = Spo;
         }
-        if (h == 0 && own) {
-            const int mC = Mv[pix];
-            const int base = NDIR * (mC - e.P2);  // S = min(base + S', MAX_COST)
-            const int bm = max(best - 1, 0), bp = min(best + 1, D - 1);
-            const bool need = Sm >= clampS || Sp >= clampS;
-            // C is stored [frame][y][x / 4][d][x % 4] on this pipeline (the
-            // cost kernel's bit-sliced mode, rows padded to 4 pixels)
-            const int prow = (int)(pix / W1), px = (int)(pix - (size_t)prow * W1);
-            const size_t cbase = ((size_t)prow * ((W1 + 3) & ~3) + (px & ~3)) * D + (px & 3);
-            auto cword = [&](int d) -> int { return need ? (int)(uint16_t)C[cbase + d * 4] : 0; };
-            auto exact = [&](int Spp, int cv) -> int {
-                const int c1 = Spp >= clampS ? cv - mC : 0;
-                return min(base + Spp + NDIR * (c1 - min(c1, 2 * e.P2)), kMaxCost);
-            };
-            const int minS = min(base + mins, kMaxCost);
-            const int Smx = exact(Sm, cword(bm)), Spx = exact(Sp, cword(bp));
-            int bst = best;
-            if (minS >= kMaxCost) bst = -1;  // no strict minimum below MAX_COST
-            const int den = max(Smx + Spx - 2 * minS, 1);
-            const int frac = ((Smx - Spx) * kDispScale + den) / (den * 2);
-            const int d16 = bst * kDispScale + (frac & -(int)(0 < bst && bst < D - 1));
-            orow[x + minX1] = (int16_t)(d16 + minD * kDispScale);
-            const int x2 = x + minX1 - bst - minD;
-            if (minS < kMaxCost && x2 >= 0 && x2 < W)
-                atomicMin(krow + x2, ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
-        }
+        if (h == 0 && own) bs_finish_pixel(C, Mv, pix, W1, W, x, best, mins, Sm, Sp, e, orow, krow);
     }
     __threadfence_block();
     __syncthreads();
-    // left-right check (OpenCV 3.4 final loop) -- reads the finished row
-    for (int x = minX1 + threadIdx.x; x < e.maxX1; x += kBsWtaThreads) {
-        const int v = orow[x];
-        if (v == INV) continue;
-        const int dlo = v >> kDispShift, dhi = (v + kDispScale - 1) >> kDispShift;
-        const int xl = x - dlo, xh = x - dhi;
-        auto d2at = [&](int xx) -> int {
-            const uint32_t kk = __hip_atomic_load(krow + xx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (kk == 0xffffffffu) return INV;
-            const int xc = 0xffff - (int)(kk & 0xffffu);
-            return xc + minX1 - xx;
-        };
-        if (0 <= xl && xl < W && 0 <= xh && xh < W) {
-            const int a = d2at(xl), b = d2at(xh);
-            if (a >= minD && abs(a - dlo) > e.disp12 && b >= minD && abs(b - dhi) > e.disp12)
-                orow[x] = (int16_t)INV;
+    bs_lr_check_row(orow, krow, W, e, kBsWtaThreads);
+}
+
+// ---------------------------------------------------------------------------
+// R->L fused with the WTA (frame batches on the strip schedule): the R->L line
+// direction's lane quads (bs_line_chains' layout) compute, right after each
+// pixel's delta, S'' = 8 C' + A_down + A_up + d_LR + d_RL for their 32
+// disparities, the argmin over the quad (bit-serial, smallest d), the minimum
+// and S''(best -+ 1), and store one packed record per pixel (best | min << 8 |
+// S''(best - 1) << 16 | S''(best + 1) << 24, grouped four pixels per 16-byte
+// store); bsgm_rl_final_kernel finishes the pixels and the LR check.  Against
+// lines + WTA this skips the R->L delta plane (written and read back) and the
+// WTA's second read of C'.
+// ---------------------------------------------------------------------------
+constexpr int kBsRG = 3;  // groups (12 steps) of operands in the register ring
+
+template <int P1, int P2>
+__global__ __launch_bounds__(64) void bsgm_rlwta_kernel(const uint32_t* __restrict__ Bc,
+                                                         const uint32_t* __restrict__ A, size_t aplane,
+                                                         const uint32_t* __restrict__ Dlr, int H, int W1,
+                                                         uint32_t* __restrict__ rec)
+{
+    const int lane = threadIdx.x;
+    const int q = lane & 3, rr = lane >> 2;
+    const int y = min((int)blockIdx.x * 16 + rr, H - 1);
+    const int f = blockIdx.y;
+    const int h = q >> 1, eo = q & 1;
+    const bool odd = eo != 0;
+    const uint32_t fill_hi = q == 3 ? kOnes : 0u, fill_lo = q == 0 ? kOnes : 0u, sh = odd ? 1u : 31u;
+    const size_t rowq = (size_t)(f * H + y) * bs::padq(W1);
+    const size_t pixrow = (size_t)(f * H + y) * W1;
+    const uint4* cgrp = (const uint4*)(Bc + bs::cq_word(rowq, 0, q));
+    const uint4* dgrp = (const uint4*)(Dlr + bs::dl_word(rowq, 0, q));
+    const uint4* adn = (const uint4*)(A + pixrow * 16 + 4 * q);  // pixel x: + 4 x
+    const uint4* aup = (const uint4*)(A + aplane + pixrow * 16 + 4 * q);
+    uint4* rgrp = (uint4*)(rec + rowq);  // group g: + g
+    const int G = (W1 + 3) >> 2;
+    const int part = W1 & 3;
+    // group of group step i (R->L, clamped: loads past the row are issued, not used)
+    auto grp = [&](int i) { return max(G - 1 - i, 0); };
+    struct Ops {
+        uint4 c[4], d[3], a[4], b[4];
+    };
+    auto load = [&](Ops& o, int i) {
+        const int g = grp(i);
+#pragma unroll
+        for (int u = 0; u < 4; u++) o.c[u] = cgrp[(size_t)g * 16 + u];
+#pragma unroll
+        for (int u = 0; u < 3; u++) o.d[u] = dgrp[(size_t)g * 12 + u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int x = min(4 * g + u, W1 - 1);
+            o.a[u] = adn[(size_t)x * 4];
+            o.b[u] = aup[(size_t)x * 4];
         }
+    };
+    const int ph = part ? 1 : 0;
+    Ops c0, ring[kBsRG];
+    if (ph) load(c0, 0);
+#pragma unroll
+    for (int j = 0; j < kBsRG; j++) {
+        load(ring[j], ph + j);
+        __builtin_amdgcn_sched_barrier(0);
     }
+    uint32_t st[3] = {0u, 0u, 0u};
+    auto w4 = [](const uint4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; };
+    auto group = [&](int i, Ops& o, int n) {
+        uint32_t rv[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int u = 3 - k;  // x = 4 g + u, descending
+            if (u < n) {
+                const uint32_t cw[4] = {o.c[u].x, o.c[u].y, o.c[u].z, o.c[u].w};
+                uint32_t nw[3], dr[3];
+                bs_quad_step<P1, P2>(st, cw, fill_hi, fill_lo, odd, sh, nw, dr);
+#pragma unroll
+                for (int b = 0; b < 3; b++) st[b] = nw[b];
+                // S'' of this lane's 32 disparities
+                const uint32_t ad[4] = {o.a[u].x, o.a[u].y, o.a[u].z, o.a[u].w};
+                const uint32_t au[4] = {o.b[u].x, o.b[u].y, o.b[u].z, o.b[u].w};
+                uint32_t dl[3];
+#pragma unroll
+                for (int b = 0; b < 3; b++) dl[b] = w4(o.d[(3 * u + b) >> 2], (3 * u + b) & 3);
+                uint32_t s5[5], d4[4], s6[6], hi[4];
+                bs::add44(ad, au, s5);  // strips <= 2 * 3 P2 = 30
+                bs::add33(dl, dr, d4);  // lines <= 2 P2 = 10
+                bs::add54(s5, d4, s6);  // all deltas <= 8 P2 = 40
+                const uint32_t top[3] = {s6[3], s6[4], s6[5]};
+                bs::add43(cw, top, hi);  // + 8 C'
+                const uint32_t S[7] = {s6[0], s6[1], s6[2], hi[0], hi[1], hi[2], hi[3]};
+                // argmin over the quad: the minimum is <= 8 P2 = 40 < 64, bit 6 is 0
+                uint32_t kk = ~S[6];
+                int mins = 0;
+#pragma unroll
+                for (int b = 5; b >= 0; b--) {
+                    const uint32_t z = bs::lop3<bs::kAndNotAB>(S[b], kk, kk);
+                    uint32_t any = z | xswap(z);
+                    any |= (uint32_t)__builtin_amdgcn_mov_dpp((int)any, 0x4E, 0xf, 0xf, true);
+                    const bool fz = any != 0u;
+                    kk = fz ? z : kk;
+                    mins |= fz ? 0 : 1 << b;
+                }
+                // smallest d among the minima (d = 64 h + 2 p + e)
+                int best = kk ? 64 * h + 2 * __builtin_ctz(kk) + eo : 1 << 20;
+                best = min(best, (int)xswap((uint32_t)best));
+                best = min(best, __builtin_amdgcn_mov_dpp(best, 0x4E, 0xf, 0xf, true));
+                // S''(best -+ 1) from the lane that holds it
+                auto sat = [&](int d) -> uint32_t {
+                    const int dq = 2 * ((d >> 6) & 1) + (d & 1), p = ((d & 63) >> 1);
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int b = 0; b < 7; b++) v |= ((S[b] >> p) & 1u) << b;
+                    return dq == q ? v : 0u;
+                };
+                uint32_t sm = sat(best - 1) | (sat(best + 1) << 8);
+                sm |= xswap(sm);
+                sm |= (uint32_t)__builtin_amdgcn_mov_dpp((int)sm, 0x4E, 0xf, 0xf, true);
+                rv[u] = (uint32_t)best | ((uint32_t)mins << 8) | (sm << 16);
+            } else {
+                rv[u] = 0u;
+            }
+        }
+        // every lane of the quad stores the same record group (unpredicated)
+        rgrp[grp(i)] = make_uint4(rv[0], rv[1], rv[2], rv[3]);
+    };
+    auto ringstep = [&](int i, int j, int n) {
+        group(i, ring[j], n);
+        load(ring[j], i + kBsRG);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    if (ph) group(0, c0, part);
+    int i = ph;
+    for (; i + kBsRG <= G; i += kBsRG) {
+#pragma unroll
+        for (int j = 0; j < kBsRG; j++) ringstep(i + j, j, 4);
+    }
+#pragma unroll
+    for (int j = 0; j < kBsRG; j++)
+        if (i + j < G) ringstep(i + j, j, 4);
+}
+
+// the per-pixel tail and the LR check of rows computed by bsgm_rlwta_kernel
+constexpr int kBsFinThreads = 256;
+__global__ __launch_bounds__(kBsFinThreads) void bsgm_rl_final_kernel(const uint32_t* __restrict__ rec,
+                                                                      const int16_t* __restrict__ C,
+                                                                      const uint16_t* __restrict__ Mv, int H, int W,
+                                                                      SgbmEff e, int16_t* __restrict__ raw,
+                                                                      uint32_t* __restrict__ keys)
+{
+    const int y = blockIdx.x, f = blockIdx.y;
+    const int W1 = e.W1;
+    int16_t* orow = raw + ((size_t)f * H + y) * W;
+    uint32_t* krow = keys + ((size_t)f * H + y) * W;
+    for (int x = threadIdx.x; x < W; x += kBsFinThreads) {
+        orow[x] = (int16_t)e.invalid;
+        krow[x] = 0xffffffffu;
+    }
+    __threadfence_block();
+    __syncthreads();
+    const uint32_t* rrow = rec + (size_t)(f * H + y) * bs::padq(W1);
+    const size_t pix0 = ((size_t)f * H + y) * W1;
+    for (int x = threadIdx.x; x < W1; x += kBsFinThreads) {
+        const uint32_t r = rrow[x];
+        bs_finish_pixel(C, Mv, pix0 + x, W1, W, x, (int)(r & 0xffu), (int)((r >> 8) & 0xffu),
+                        (int)((r >> 16) & 0xffu), (int)(r >> 24), e, orow, krow);
+    }
+    __threadfence_block();
+    __syncthreads();
+    bs_lr_check_row(orow, krow, W, e, kBsFinThreads);
 }
 
 }  // namespace
@@ -1001,11 +1186,13 @@ int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16
                      (rc = check_hip(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0), "fork wait"))))
             return rc;
         hipStream_t ls = side ? ctx->aux : s;
+        // fused: only L->R here, R->L runs with the WTA (bsgm_rlwta_kernel)
+        const bool fuse = ctx->bs_fuse != 0;
         auto lines = [&]() -> int {
             StageTimer tl(ctx, kStageLines, ls);
             const char* pv = std::getenv("MVSV_BS_LPROBE");
-            hipLaunchKernelGGL((bsgm_lines4_kernel<2, 5>), dim3((H + 15) / 16, n, 2), dim3(64), 0, ls, Bv, Dv,
-                               dplane, H, e.W1, pv ? std::atoi(pv) : 0);
+            hipLaunchKernelGGL((bsgm_lines4_kernel<2, 5>), dim3((H + 15) / 16, n, fuse ? 1 : 2), dim3(64), 0, ls,
+                               Bv, Dv, dplane, H, e.W1, pv ? std::atoi(pv) : 0);
             return check_hip(ctx, hipGetLastError(), "bit-sliced line kernel");
         };
         if (side && (rc = lines())) return rc;
@@ -1025,6 +1212,16 @@ int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16
             return rc;
     }
     StageTimer tm(ctx, kStageFinal);
+    if (ctx->bs_fuse) {
+        // per-pixel records in the (unused) R->L plane's space
+        uint32_t* rec = Dv + dplane;
+        hipLaunchKernelGGL((bsgm_rlwta_kernel<2, 5>), dim3((H + 15) / 16, n), dim3(64), 0, s, Bv, Av, aplane, Dv,
+                           H, e.W1, rec);
+        if ((rc = check_hip(ctx, hipGetLastError(), "bit-sliced R->L + WTA kernel"))) return rc;
+        hipLaunchKernelGGL(bsgm_rl_final_kernel, dim3(H, n), dim3(kBsFinThreads), 0, s, rec, Cv, Mv, H, W, e, raw,
+                           (uint32_t*)ctx->keys.ptr);
+        return check_hip(ctx, hipGetLastError(), "bit-sliced final kernel");
+    }
     hipLaunchKernelGGL(bsgm_wta_kernel<false>, dim3(H, n), dim3(kBsWtaThreads), 0, s, Bv, Av, aplane, Dv, dplane, Cv, Mv, H,
                        W, e, raw, (uint32_t*)ctx->keys.ptr);
     return check_hip(ctx, hipGetLastError(), "bit-sliced WTA kernel");

@@ -288,6 +288,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
     if (const char* v = std::getenv("MVSV_BITSLICE")) c->bitslice = std::atoi(v) != 0;
     if (const char* v = std::getenv("MVSV_BS_SERIAL")) c->bs_serial = std::atoi(v) != 0;
     if (const char* v = std::getenv("MVSV_COST_XCD")) c->cost_xcd = std::atoi(v) != 0;
+    if (const char* v = std::getenv("MVSV_BS_FUSE")) c->bs_fuse = std::atoi(v) != 0;
     if (const char* v = std::getenv("MVSV_BS_GROUPS")) {
         const int g = std::atoi(v);
         c->bs_groups = (g == 1 || g == 4 || g == 5) ? g : 2;

@@ -128,6 +128,7 @@ struct mvsv_ctx {
     int bitslice = 1;    // bit-sliced MODE_HH paths where they apply (MVSV_OPT_BITSLICE, env MVSV_BITSLICE)
     int bs_groups = 2;   // column groups (3 direction waves each) per bit-sliced strip: 1, 2, 4, 5 (MVSV_BS_GROUPS)
     int cost_xcd = 1;    // cost kernel: whole row bands per XCD (MVSV_COST_XCD=0: blockIdx order, A/B)
+    int bs_fuse = 1;     // bit-sliced batches: R->L lines fused with the WTA (MVSV_BS_FUSE=0: separate, A/B)
     int bs_serial = 0;   // 1: bit-sliced line kernel after the strips on the context stream (MVSV_BS_SERIAL, A/B)
     int bm2 = 1;     // StereoBM: disparities-on-lanes match kernel where blockSize <= 21, D <= 128
     int bm_ty = 0;   // its tile height (0 = chosen per launch); MVSV_BM_TY for A/B runs

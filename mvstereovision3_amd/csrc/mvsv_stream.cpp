@@ -342,6 +342,7 @@ static void copy_options(mvsv_ctx* d, const mvsv_ctx* s)
     d->bs_groups = s->bs_groups;
     d->bs_serial = s->bs_serial;
     d->cost_xcd = s->cost_xcd;
+    d->bs_fuse = s->bs_fuse;
 }
 
 int mvsv_stream_set_inflight(mvsv_stream* st, int n)

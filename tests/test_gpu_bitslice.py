@@ -50,14 +50,17 @@ def test_bitslice_hh_forced(gpu, mvsv, oracle, case, bits, sched):
     assert np.array_equal(got, want), f"bitslice={bits} sched={sched} variant={variant} {kw}: " + report(got, want)
 
 
-@pytest.mark.parametrize("groups", ["1", "2", "4", "5", "2-side"])
+@pytest.mark.parametrize("groups", ["1", "2", "4", "5", "2-serial", "2-nofuse"])
 def test_bitslice_strip_groups(gpu, mvsv, oracle, groups, monkeypatch):
     """Every strip width (column groups per strip) on a 3-frame device batch;
-    4-side: the line kernel beside the strips on the aux stream."""
+    -serial: the L->R lines after the strips on the context stream instead of
+    beside them; -nofuse: both line directions in the line kernel and the
+    separate WTA instead of R->L fused with the WTA."""
     from mvstereovision3_amd import _lib
     torch = gpu
     monkeypatch.setenv("MVSV_BS_GROUPS", groups.split("-")[0])
-    monkeypatch.setenv("MVSV_BS_SERIAL", "0" if groups.endswith("side") else "1")
+    monkeypatch.setenv("MVSV_BS_SERIAL", "1" if groups.endswith("serial") else "0")
+    monkeypatch.setenv("MVSV_BS_FUSE", "0" if groups.endswith("nofuse") else "1")
     monkeypatch.setenv("MVSV_PATH_SCHEDULE", "1")
     ctx = _lib.Context(0)  # a fresh context reads the environment
     rng = np.random.default_rng(5200 + len(groups) + int(groups[0]))
