@@ -54,7 +54,7 @@ if ROOT not in sys.path:
 SEED0 = 0x5EED0000
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SGBM_YML = os.path.join(ROOT, "tests", "golden", "configs", "sgbm.yml")
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
 PMC_FILE = os.path.join(PROFILE_DIR, "pmc_traffic.json")  # tools/pmc_traffic.py
 SQ_FILE = os.path.join(PROFILE_DIR, "sq_summary.json")    # tools/sq_summary.py
 KERNEL_SOURCES = os.path.join(ROOT, "mvstereovision3_amd", "csrc")
@@ -132,9 +132,9 @@ def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True, res=False, bits=F
     plane (0.5 B per cost, written by the cost kernel beside C) instead of C.
     bits = the bit-sliced MODE_HH pipeline (mvsv_bsgm.hip): the
     cost kernel writes C (read back only at best -+ 1) and the 4-bit C' planes,
-    the strip passes read C' and write a 4-bit plane each, the two line
-    directions read C' and write 3-bit planes, the WTA reads C', every plane and
-    the gathered costs.
+    the strip passes read C' and write a 4-bit plane each, the L->R lines read
+    C' and write a 3-bit plane, the R->L lines fused with the WTA read C', the
+    three planes and the gathered costs.
     """
     cells = W1 * H * D
     px = W * H
@@ -142,16 +142,17 @@ def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True, res=False, bits=F
     cin = 0.5 if res else 2
     if bits:
         strip_b = F * cells * 2 * (0.5 + 0.5)
-        lines_b = F * cells * 2 * (0.5 + 0.375)
+        lines_b = F * cells * (0.5 + 0.375)  # L->R only: R->L runs with the WTA
         return {
             "prefilter": F * (2 * px + 2 * 8 * px),
             "cost_volume": F * (2 * 8 * px + 2.5 * cells + 2 * W1 * H),
             "path_aggregation": strip_b + lines_b,
             "path_strips": strip_b,
             "path_lines": lines_b,
-            # C', two strip planes, two line planes; minimum, gathered costs,
-            # raw map and right-view keys per pixel
-            "final_wta_lr": F * (cells * (0.5 + 2 * 0.5 + 2 * 0.375) + W1 * H * (2 + 8) + 6 * px),
+            # R->L + WTA: C', two strip planes, the L->R plane, a 4-byte record
+            # per pixel written and read back; the finish: minimum, gathered
+            # costs, raw map and right-view keys per pixel
+            "final_wta_lr": F * (cells * (0.5 + 2 * 0.5 + 0.375) + W1 * H * (8 + 2 + 8) + 6 * px),
             "post_filters": F * 4 * px,
         }.get(stage, 0)
     if strips:

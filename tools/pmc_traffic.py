@@ -20,6 +20,8 @@ from bench import kernel_source_sha  # noqa: E402
 
 STAGES = [("sgbm_tri_kernel", "path_strips"), ("bsgm_strip_kernel", "path_strips"),
           ("bsgm_lines4_kernel", "path_lines"), ("bsgm_wta_kernel", "final_wta_lr"),
+          ("bsgm_rlwta_kernel", "final_wta_lr"), ("bsgm_rl_final_kernel", "final_wta_lr"),
+          ("bsgm_dir_kernel", "path_aggregation"),
           ("sgbm_path16_kernel", "path_lines"),
           ("sgbm_path_kernel", "path_aggregation"), ("sgbm_cost_fixup", "cost_fixup"),
           ("sgbm_cost", "cost_volume"), ("sgbm_final", "final_wta_lr"),
@@ -50,17 +52,22 @@ def per_dispatch(path, counter):
 def main(fetch_csv, write_csv, workload, out):
     f, fn = per_dispatch(fetch_csv, "FETCH_SIZE")
     w, wn = per_dispatch(write_csv, "WRITE_SIZE")
-    acc = defaultdict(lambda: {"launches": 0, "fetch_kib": 0.0})
-    accw = defaultdict(lambda: {"launches": 0, "write_kib": 0.0})
+    # a stage's launches = the dispatch count of its most frequent kernel (one
+    # per step), so a stage of several kernels (post filters, the fused R->L +
+    # WTA and its finishing pass) reports its bytes per step
+    acc = defaultdict(lambda: {"launches": 0, "fetch_kib": 0.0, "per_kernel": defaultdict(int)})
+    accw = defaultdict(lambda: {"launches": 0, "write_kib": 0.0, "per_kernel": defaultdict(int)})
     for d, v in f.items():
         st = stage_of(fn[d])
         if st:
-            acc[st]["launches"] += 1
+            acc[st]["per_kernel"][fn[d]] += 1
+            acc[st]["launches"] = max(acc[st]["per_kernel"].values())
             acc[st]["fetch_kib"] += v
     for d, v in w.items():
         st = stage_of(wn[d])
         if st:
-            accw[st]["launches"] += 1
+            accw[st]["per_kernel"][wn[d]] += 1
+            accw[st]["launches"] = max(accw[st]["per_kernel"].values())
             accw[st]["write_kib"] += v
     stages = {}
     for st in sorted(set(acc) | set(accw)):

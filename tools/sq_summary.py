@@ -36,6 +36,8 @@ XCDS = 8
 
 STAGES = [("sgbm_tri_kernel", "path_strips"), ("bsgm_strip_kernel", "path_strips"),
           ("bsgm_lines4_kernel", "path_lines"), ("bsgm_wta_kernel", "final_wta_lr"),
+          ("bsgm_rlwta_kernel", "final_wta_lr"), ("bsgm_rl_final_kernel", "final_wta_lr"),
+          ("bsgm_dir_kernel", "path_aggregation"),
           ("sgbm_path16_kernel", "path_lines"),
           ("sgbm_pathdirs16_kernel", "path_aggregation"), ("sgbm_path_kernel", "path_aggregation"),
           ("sgbm_cost_fixup", "cost_fixup"), ("sgbm_cost", "cost_volume"),
