@@ -39,6 +39,11 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--large", type=int, default=0,
                     help="extra SGBM cases at 640x480 / 1280x960 with 4-8 frame batches")
+    ap.add_argument("--bits", type=int, default=0,
+                    help="SGBM cases in the bit-sliced regime (MODE_HH, D 128, P1 2 / P2 5, "
+                         "uniquenessRatio 0): random shapes, batches, schedules, bit-sliced on / off")
+    ap.add_argument("--bits-large", type=int, default=0,
+                    help="bit-sliced-regime cases at 640x480 / 1280x960, 1-8 frames")
     a = ap.parse_args()
     import torch
 
@@ -129,6 +134,51 @@ def main():
             jobs.append((f"large #{i} frame {j}/{n} {W}x{H} {kw}", got[j], pool.submit(pyoracle.sgbm, L, R, p)))
     _lib.set_option(_lib.OPT_STRIP_TICKETS, 1)
     _lib.set_option(_lib.OPT_COST_RESIDUAL, 1)
+
+    # the bit-sliced MODE_HH pipeline (round 5): strips + fused R->L / WTA for
+    # batches, the side-by-side chains for small launches, forced off
+    for i in range(a.bits + a.bits_large):
+        large = i >= a.bits
+        if large:
+            W, H = (640, 480) if rng.integers(0, 2) else (1280, 960)
+            n = int(rng.choice([1, 2, 4, 8])) if W == 640 else int(rng.choice([1, 2, 3]))
+        else:
+            n = int(rng.choice([1, 1, 2, 3, 5]))
+            H, W = int(rng.integers(8, 160)), int(rng.integers(150, 420))
+        minD = int(rng.integers(-8, 8))
+        if W + min(minD, 0) - max(minD + 128, 0) < 1:
+            continue
+        kw = dict(minDisparity=minD, numDisparities=128, blockSize=int(rng.choice([0, 1, 3, 5, 9, 13, 15])),
+                  P1=int(rng.choice([0, 2])), P2=int(rng.choice([0, 5])), disp12MaxDiff=int(rng.integers(-1, 4)),
+                  preFilterCap=int(rng.choice([0, 15, 31, 63])), uniquenessRatio=0,
+                  speckleWindowSize=int(rng.choice([0, 0, 20, 150])), speckleRange=int(rng.choice([1, 2, 4])), mode=1)
+        variant = int(rng.integers(0, 4))
+        sched = int(rng.choice([0, 0, 1, 2]))
+        bits = int(rng.choice([1, 1, 1, 0]))
+        m = mvsv.StereoSGBM.create(**kw)
+        m.setVariant(variant)
+        _lib.set_option(_lib.OPT_PATH_SCHEDULE, sched)
+        _lib.set_option(_lib.OPT_BITSLICE, bits)
+        if large:
+            pairs = [mvsv.synth_pair(int(rng.integers(0, 1 << 30)), W, H, max(minD, 0), 128) for _ in range(n)]
+        else:
+            pairs = [rand_pair(rng, H, W, int(rng.integers(0, 64)), int(rng.integers(0, 3))) for _ in range(n)]
+        try:
+            Lb = torch.from_numpy(np.stack([q[0] for q in pairs])).to(dev)
+            Rb = torch.from_numpy(np.stack([q[1] for q in pairs])).to(dev)
+            out = torch.empty((n, H, W), dtype=torch.int16, device=dev)
+            m.compute(Lb, Rb, out)
+            got = out.cpu().numpy()
+        except mvsv.MvsvError as ex:
+            print(f"GPU ERROR bits #{i} {H}x{W} {kw}: {ex}", flush=True)
+            bad += 1
+            continue
+        p = {k: v for k, v in m.params().items() if k != "variant"}
+        for j, (L, R) in enumerate(pairs):
+            tag = f"bits #{i} frame {j}/{n} {H}x{W} {kw} variant={variant} sched={sched} bitslice={bits}"
+            jobs.append((tag, got[j], pool.submit(pyoracle.sgbm, L, R, p, variant)))
+    _lib.set_option(_lib.OPT_PATH_SCHEDULE, 0)
+    _lib.set_option(_lib.OPT_BITSLICE, 1)
 
     for i in range(a.bm):
         H, W = int(rng.integers(24, 200)), int(rng.integers(80, 400))
