@@ -859,8 +859,8 @@ __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t*
 #pragma unroll
             for (int b = 0; b < 7; b++) {
                 const uint32_t wv = eb ? S[0][b] : S[1][b];
-                Sm |= (int)((wv >> pm) & 1u) << b;
-                Sp |= (int)((wv >> pp) & 1u) << b;
+                Sm |= (int)(__builtin_amdgcn_ubfe(wv, (uint32_t)pm, 1u) << b);
+                Sp |= (int)(__builtin_amdgcn_ubfe(wv, (uint32_t)pp, 1u) << b);
             }
             const int Smo = (int)xswap((uint32_t)Sm), Spo = (int)xswap((uint32_t)Sp);
             if (((best - 1) >> 6) != h) Sm = Smo;
@@ -981,7 +981,8 @@ __global__ __launch_bounds__(64) void bsgm_rlwta_kernel(const uint32_t* __restri
                     const int dq = 2 * ((d >> 6) & 1) + (d & 1), p = ((d & 63) >> 1);
                     uint32_t v = 0;
 #pragma unroll
-                    for (int b = 0; b < 7; b++) v |= ((S[b] >> p) & 1u) << b;
+                    // one v_bfe + one v_lshl_or per bit
+                    for (int b = 0; b < 7; b++) v |= __builtin_amdgcn_ubfe(S[b], (uint32_t)p, 1u) << b;
                     return dq == q ? v : 0u;
                 };
                 uint32_t sm = sat(best - 1) | (sat(best + 1) << 8);
