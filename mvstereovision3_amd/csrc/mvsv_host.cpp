@@ -476,6 +476,23 @@ size_t mvsv_sgbm_workspace_bytes(int n, int W, int H, const mvsv_sgbm_params* p)
     if (e.speckle_window > 0) b += (size_t)n * frame * (4 + 4 + 4 + 2 + 4) + 4;
     // cost residual plane + per-pixel minimum (MVSV_OPT_COST_RESIDUAL, where exact)
     if (3 * e.P2 <= 15 && e.D <= 128 && e.W1 > 0) b += (size_t)n * e.W1 * H * (e.D / 2 + 2);
+    // the BT interval planes of both views (u64 per pixel each)
+    b += (size_t)n * frame * 16;
+    // the bit-sliced pipeline (MVSV_OPT_BITSLICE, default on):
+    // rows padded to 4 pixels, delta planes beyond the accumulator budget above
+    // (eight 48-byte planes side by side for small launches), strip boundary
+    // granules (2 passes x strips of 64 U-columns x H rows x 36 u64)
+    const long bsz = 2L * e.SW2 + 1;
+    const bool bs_regime = e.fullDP && e.D == 128 && e.P1 == 2 && e.P2 == 5 && e.uniq == 0 && e.W1 > 0 &&
+                           (long)e.P2 + bsz * bsz * (2L * e.ftzero + 63) + e.P2 <= 32767;
+    if (bs_regime) {
+        const size_t W1q = (size_t)(e.W1 + 3) & ~(size_t)3;
+        b += (size_t)n * H * (W1q - e.W1) * (e.D * 2 + 64);               // padded C and C'
+        const size_t side = (size_t)n * H * W1q * 8 * 48, acc = (size_t)n * vol;
+        if (side > acc) b += side - acc;
+        const size_t nstrips = ((size_t)e.W1 + H - 1 + 63) / 64;
+        b += 2 * (size_t)n * nstrips * H * 36 * 8;
+    }
     return b;
 }
 
