@@ -91,3 +91,33 @@ def test_bitslice_option_range(gpu):
     for bad in (-1, 2):
         with pytest.raises(_lib.MvsvError):
             _lib.set_option(_lib.OPT_BITSLICE, bad)
+
+
+@pytest.mark.parametrize("shape", [(1, 480, 640), (8, 240, 640)])
+def test_bitslice_workspace_bound(gpu, mvsv, shape):
+    """mvsv_sgbm_workspace_bytes bounds what a fresh context allocates for one
+    bit-sliced call (side by side for the single frame, strips for the batch)."""
+    import ctypes
+    from mvstereovision3_amd import _lib
+    torch = gpu
+    n, H, W = shape
+    m = mvsv.StereoSGBM.create(minDisparity=1, numDisparities=128, blockSize=13, P1=0, P2=0,
+                               uniquenessRatio=0, speckleWindowSize=150, speckleRange=2, mode=1)
+    est = _lib.lib().mvsv_sgbm_workspace_bytes(n, W, H, ctypes.byref(m._params))
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5300 + n)
+    L = torch.from_numpy(rng.integers(0, 256, (n, H, W), dtype=np.uint8)).to(dev)
+    R = torch.roll(L, -20, dims=2).contiguous()
+    out = torch.empty((n, H, W), dtype=torch.int16, device=dev)
+    torch.cuda.synchronize()
+    ctx = _lib.Context(0)
+    try:
+        free0 = torch.cuda.mem_get_info()[0]
+        with _lib.use_context(ctx):
+            m.compute(L, R, out)
+            _lib.synchronize(0)
+        used = free0 - torch.cuda.mem_get_info()[0]
+    finally:
+        ctx.close()
+    # allocation granularity / runtime slack: 64 MB
+    assert used <= est + (64 << 20), f"context used {used} B, workspace estimate {est} B"
