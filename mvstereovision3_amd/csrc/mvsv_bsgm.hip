@@ -163,7 +163,7 @@ __global__ __launch_bounds__(BsStripCfg<NG>::kThreads) void bsgm_strip_kernel(
     int H, int W1, int npass,
     unsigned long long* __restrict__ bnd, unsigned epoch, int nframes, int* __restrict__ status,
     unsigned spin_limit, int* __restrict__ report, long long ticket0, unsigned long long* __restrict__ stats,
-    int nowait)
+    int)
 {
     using Cfg = BsStripCfg<NG>;
     constexpr int SW = Cfg::kSW, NCOL = Cfg::kCols;
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(BsStripCfg<NG>::kThreads) void bsgm_strip_kernel(
     unsigned long long st_t0 = stats ? __builtin_amdgcn_s_memtime() : 0ull, st_spin = 0, st_n = 0;
     auto bconsume = [&](int t, int buf, unsigned long long g) {
         const bool need = bvalid(t);
-        bool ok = nowait || !need || (unsigned)(g >> 32) == epoch;
+        bool ok = !need || (unsigned)(g >> 32) == epoch;
         if (!__all(ok)) {
             const unsigned long long sp0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
             unsigned spins = 0;
@@ -455,12 +455,13 @@ __global__ __launch_bounds__(BsStripCfg<NG>::kThreads) void bsgm_strip_kernel(
 // contiguous bytes of C' (kBsLG groups ahead, in registers) and stores 48 of
 // deltas -- with one 16-byte load and one 12-byte store per step (a load
 // instruction then covering 16 rows x 64 bytes) the pass measured 0.50 ms of
-// which 0.28 went to those loads and 0.14 to those stores (MVSV_BS_LPROBE).
+// which 0.28 went to those loads and 0.14 to those stores (probes with the
+// loads from one cached row / the stores to one slot, profiles/r05/README.md).
 constexpr int kBsLG = 8;
 
 template <int P1, int P2>
 __device__ __forceinline__ void bs_line_chains(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dl,
-                                               size_t plane_words, int H, int W1, int probe, bool rl)
+                                               size_t plane_words, int H, int W1, bool rl)
 {
     const int lane = threadIdx.x;
     const int q = lane & 3, rr = lane >> 2;
@@ -478,10 +479,9 @@ __device__ __forceinline__ void bs_line_chains(const uint32_t* __restrict__ Bc, 
         uint4* dgrp = (uint4*)(Dl + (RL ? plane_words : 0) + bs::dl_word(rowq, 0, q));
         // group of the i-th group step (clamped: loads past the row are issued, not used)
         auto grp = [&](int i) { return RL ? max(G - 1 - i, 0) : min(i, G - 1); };
-        auto lgrp = [&](int i) { return (probe & 2) ? (i & 1) : grp(i); };
         uint4 cr[kBsLG][4];
         auto load = [&](int j, int i) {
-            const uint4* p = cgrp + (size_t)lgrp(i) * 16;
+            const uint4* p = cgrp + (size_t)grp(i) * 16;
 #pragma unroll
             for (int u = 0; u < 4; u++) cr[j][u] = p[u];
         };
@@ -491,7 +491,7 @@ __device__ __forceinline__ void bs_line_chains(const uint32_t* __restrict__ Bc, 
         uint4 c0[4];
         if (ph) {
 #pragma unroll
-            for (int u = 0; u < 4; u++) c0[u] = cgrp[(size_t)lgrp(0) * 16 + u];
+            for (int u = 0; u < 4; u++) c0[u] = cgrp[(size_t)grp(0) * 16 + u];
         }
         // (issued in slot order: the loop head's wait for slot 0 assumes it)
 #pragma unroll
@@ -521,7 +521,7 @@ __device__ __forceinline__ void bs_line_chains(const uint32_t* __restrict__ Bc, 
                     for (int b = 0; b < 3; b++) dv[3 * u + b] = 0u;
                 }
             }
-            uint4* o = dgrp + (size_t)((probe & 1) ? 0 : grp(i)) * 12;
+            uint4* o = dgrp + (size_t)grp(i) * 12;
             o[0] = make_uint4(dv[0], dv[1], dv[2], dv[3]);
             o[1] = make_uint4(dv[4], dv[5], dv[6], dv[7]);
             o[2] = make_uint4(dv[8], dv[9], dv[10], dv[11]);
@@ -559,9 +559,9 @@ __device__ __forceinline__ void bs_line_chains(const uint32_t* __restrict__ Bc, 
 
 template <int P1, int P2>
 __global__ __launch_bounds__(64) void bsgm_lines4_kernel(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dl,
-                                                          size_t plane_words, int H, int W1, int probe)
+                                                          size_t plane_words, int H, int W1)
 {
-    bs_line_chains<P1, P2>(Bc, Dl, plane_words, H, W1, probe, blockIdx.z != 0);
+    bs_line_chains<P1, P2>(Bc, Dl, plane_words, H, W1, blockIdx.z != 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -657,7 +657,7 @@ __global__ __launch_bounds__(64) void bsgm_dir_kernel(const uint32_t* __restrict
 {
     if (blockIdx.z >= 6) {
         if ((int)blockIdx.x * 16 < H)
-            bs_line_chains<P1, P2>(Bc, Dp + 6 * plane_words, plane_words, H, W1, 0, blockIdx.z == 7);
+            bs_line_chains<P1, P2>(Bc, Dp + 6 * plane_words, plane_words, H, W1, blockIdx.z == 7);
         return;
     }
     const int pass = blockIdx.z / 3, slot = blockIdx.z - 3 * pass;
@@ -1083,14 +1083,12 @@ static int launch_bs_strips(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const
     const unsigned epoch = ctx->tri_epoch;
     const dim3 grid(nstrips * npass * n);
     const bool tickets = ctx->strip_tickets != 0;
-    // MVSV_BS_STATS: per-strip spans and hand-off spin time on stderr;
-    // MVSV_BS_NOWAIT: timing probe without the hand-off waits (maps wrong)
+    // MVSV_BS_STATS: per-strip spans and hand-off spin time on stderr
     unsigned long long* stats = nullptr;
     if (std::getenv("MVSV_BS_STATS")) {
         (void)hipMalloc(&stats, (size_t)grid.x * 64);
         (void)hipMemset(stats, 0, (size_t)grid.x * 64);
     }
-    const bool nowait = std::getenv("MVSV_BS_NOWAIT") != nullptr;
     // one strip block per CU: dynamic LDS past half the CU's 160 KiB (a second
     // strip block on the same CU makes that CU's strips, and every strip left of
     // them in the chain, step at half speed -- 2-group strips measured 1.17 ms
@@ -1107,7 +1105,7 @@ static int launch_bs_strips(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const
     hipLaunchKernelGGL((bsgm_strip_kernel<NG, 2, 5>), grid, dim3(Cfg::kThreads), lds, ctx->stream, Bv, Av,
                        aplane, dummy, H, e.W1, npass, (unsigned long long*)ctx->bs_bnd.ptr, epoch, n,
                        (int*)ctx->status.ptr, ctx->spin_limit, ctx->report_target,
-                       tickets ? (long long)ctx->tri_tickets : -1ll, stats, nowait ? 1 : 0);
+                       tickets ? (long long)ctx->tri_tickets : -1ll, stats, 0);
     rc = check_hip(ctx, hipGetLastError(), "bit-sliced strip kernel");
     if (rc == MVSV_OK && tickets) ctx->tri_tickets += grid.x;
     if (stats) {
@@ -1191,9 +1189,8 @@ int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16
         const bool fuse = ctx->bs_fuse != 0;
         auto lines = [&]() -> int {
             StageTimer tl(ctx, kStageLines, ls);
-            const char* pv = std::getenv("MVSV_BS_LPROBE");
             hipLaunchKernelGGL((bsgm_lines4_kernel<2, 5>), dim3((H + 15) / 16, n, fuse ? 1 : 2), dim3(64), 0, ls,
-                               Bv, Dv, dplane, H, e.W1, pv ? std::atoi(pv) : 0);
+                               Bv, Dv, dplane, H, e.W1);
             return check_hip(ctx, hipGetLastError(), "bit-sliced line kernel");
         };
         if (side && (rc = lines())) return rc;
