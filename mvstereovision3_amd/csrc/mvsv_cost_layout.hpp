@@ -74,6 +74,26 @@ MVSV_HD inline Cost2Layout cost2_layout(int D, int SW2, int TY)
     return c;
 }
 
+// Ring slots of the vertical window kept in LDS instead of registers (slots
+// RR .. NR - 1, RR = NR - this; one uint4 per thread and slot after the
+// layout's buffers).  Large windows of the D = 128 / 256 kernels otherwise
+// exceed 128 VGPRs (4 waves per SIMD) and the compiler spills ring slots to
+// scratch, whose evicted lines reach HBM (tools/kernel_resources.py audits it).
+MVSV_HD constexpr int cost2_lds_ring_slots(int nr, int stg, int ppc)
+{
+    // (register slots 8 for D = 128 up to blockSize 13, 10 at 15 so that two
+    // blocks still fit a CU's LDS; 12 for D = 256 -- tools/kernel_resources.py)
+    return stg != 1 ? 0
+           : ppc == 64  ? (nr > 13 ? nr - 10 : nr > 8 ? nr - 8 : 0)
+           : ppc == 128 ? (nr > 12 ? nr - 12 : 0)
+                        : 0;
+}
+MVSV_HD inline size_t cost2_ring_offset(const Cost2Layout& l) { return (l.bytes + 15) & ~(size_t)15; }
+MVSV_HD inline size_t cost2_total_bytes(const Cost2Layout& l, int nr, int stg, int ppc)
+{
+    return cost2_ring_offset(l) + (size_t)cost2_lds_ring_slots(nr, stg, ppc) * kCost2Threads * 16;
+}
+
 MVSV_HD inline int cost2_clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // One TX x TY tile of cost columns [x0, x0+TX) x rows [y0, y1): the left image

@@ -562,6 +562,9 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                     const uint32_t c1 =
                         bt_cost2(pl4[2 * CLC * k + 1], pl2[2 * CLC * k + 1], qb4[CLC * k], qb2[CLC * k]);
                     pp[CLC * k] = make_uint2(c0, c1);
+#if MVSV_COST2_PIX_FENCE
+                    __builtin_amdgcn_sched_barrier(0);
+#endif
                 }
                 return;
             }
@@ -597,13 +600,20 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
         }
     };
 
-    uint32_t csum[kCost2Run], ring[NR][kCost2Run];
+    // the vertical window's ring of horizontal sums: slots 0 .. RR - 1 in
+    // registers, RR .. NR - 1 in LDS (cost2_lds_ring_slots; this thread's own
+    // words, so no barrier)
+    constexpr int RL = cost2_lds_ring_slots(NR, STG, PPC), RR = NR - RL;
+    uint4* ringl = (uint4*)(smem + cost2_ring_offset(lay)) + tid;
+    uint32_t csum[kCost2Run], ring[RR][kCost2Run];
 #pragma unroll
     for (int i = 0; i < kCost2Run; i++) {
         csum[i] = 0;
 #pragma unroll
-        for (int s = 0; s < NR; s++) ring[s][i] = 0;
+        for (int s = 0; s < RR; s++) ring[s][i] = 0;
     }
+#pragma unroll
+    for (int s = 0; s < RL; s++) ringl[s * kCost2Threads] = make_uint4(0, 0, 0, 0);
 
     const int vstart = y0 - SH2;
     const int nrows = (y1 - y0) + 2 * SH2;
@@ -642,6 +652,10 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
             pix_row(buf);
             __syncthreads();  // pix[buf] complete; staging of row k+1 visible
             if (worker) {
+                const bool lslot = s >= RR;
+                const int sr = lslot ? 0 : s;
+                uint4 lold = make_uint4(0, 0, 0, 0);
+                if (lslot) lold = ringl[(s - RR) * kCost2Threads];
                 // the thread's NR + RUN - 1 window columns: b64 loads, all in flight
                 constexpr int NV = NR + kCost2Run - 1;  // even
                 const uint2* pr = (const uint2*)((const uint32_t*)(smem + lay.off_pix + (buf ? lay.pstride : 0)) +
@@ -661,21 +675,33 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                 // subtracts a term the sum holds)
                 for (int q = 0; q < NR; q++) h = add2_nc(h, wv[q]);
                 const bool emit = k >= NR - 1;
-                uint32_t* orow = obase + (size_t)k * ostride;
+                // the step's row offsets from an opaque copy of k: otherwise the
+                // compiler keeps one set of output addresses per unrolled step
+                // live across the loop (registers the ring needs)
+                int ko = k;
+#if MVSV_COST2_OPAQUE_K
+                asm volatile("" : "+s"(ko));
+#endif
+                uint32_t* orow = obase + (size_t)ko * ostride;
                 // MODE_HH: OpenCV 3.4 leaves P2 in the rows it never recomputes
                 // (y >= H - SH2) and in column x = 0 of rows y >= 1
                 const int yo = y0 - 2 * SH2 + k;
                 const bool pin_row = hh_pin && yo >= ybot;
                 const bool pin_x0 = hh_pin && !fix_x0 && yo >= 1 && x0 + tx0 == 0;
-                uint32_t ov[kCost2Run];
+                uint32_t ov[kCost2Run], hv[kCost2Run];
 #pragma unroll
                 for (int i = 0; i < kCost2Run; i++) {
                     if (i > 0) h = sub2_nb(add2_nc(h, wv[i + NR - 1]), wv[i - 1]);
-                    csum[i] = add2_nc(sub2_nb(csum[i], ring[s][i]), h);
-                    ring[s][i] = h;
+                    const uint32_t lo_i = i == 0 ? lold.x : i == 1 ? lold.y : i == 2 ? lold.z : lold.w;
+                    csum[i] = add2_nc(sub2_nb(csum[i], lslot ? lo_i : ring[sr][i]), h);
+                    if (lslot)
+                        hv[i] = h;
+                    else
+                        ring[sr][i] = h;
                     const bool pin = pin_row || (i == 0 && pin_x0);
                     ov[i] = pin ? p2x2 : pk_add_u16(p2x2, csum[i]);
                 }
+                if (lslot) ringl[(s - RR) * kCost2Threads] = make_uint4(hv[0], hv[1], hv[2], hv[3]);
                 // every column of the wave inside the image (all but the last
                 // tile column): unpredicated stores
                 const bool full = __all(nout == kCost2Run);
@@ -746,7 +772,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                             // the four-pixel group of the wave's columns (mvsv_bitslice.hpp
                             // cq_word): word (q' = 2 h + e) * 16 + c * 4 + b
                             const int qw = (2 * (p >> 5) + ((q & 7) >> 2)) * 16 + c * 4 + (q & 3);
-                            if (full || c < nout) bq[(ptrdiff_t)k * W1q * 16 + qw] = tw;
+                            if (full || c < nout) bq[(ptrdiff_t)ko * W1q * 16 + qw] = tw;
                             // C is read only for the WTA's C(best -+ 1) gathers, so it
                             // is stored [frame][y][x / 4][d][x % 4] (rows padded to
                             // a multiple of 4 pixels, read by mvsv_bsgm.hip bsgm_wta_kernel):
@@ -755,7 +781,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                             // wave's 1 KiB as one run
                             // (a wave wholly right of W1 -- nout <= 0 -- would land in
                             // the next row)
-                            if (nout > 0) cq[(ptrdiff_t)k * W1q * 16] = make_uint4(Plo01, Plo23, Phi01, Phi23);
+                            if (nout > 0) cq[(ptrdiff_t)ko * W1q * 16] = make_uint4(Plo01, Plo23, Phi01, Phi23);
                         }
                     }
                     if (Rv) {
@@ -3240,25 +3266,25 @@ static int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int
     if (ctx->cost2 && e.SH2 <= 7 && e.SW2 == e.SH2) {
         const Cost2Layout l2 = cost2_layout(e.D, e.SW2, TY);
         const int items = 2 * l2.NX + e.D - 1;
-        if (l2.CL >= 1 && items <= kCost2Threads * 2 &&
-            l2.bytes <= 160 * 1024) {
+        const bool two = items > kCost2Threads;
+        // numDisparities 128 / 256: the pair count is a compile-time
+        // constant (unrolled pixel-cost loop, immediate LDS offsets)
+        const int ppc = !ctx->cost_fixed_pp ? 0 : l2.PP == 64 ? 64 : (l2.PP == 128 ? 128 : 0);
+        const size_t lbytes = cost2_total_bytes(l2, 2 * e.SH2 + 1, two ? 2 : 1, ppc);
+        if (l2.CL >= 1 && items <= kCost2Threads * 2 && lbytes <= 160 * 1024) {
             dim3 grid2((e.W1 + l2.TX - 1) / l2.TX, (H + TY - 1) / TY, n);
             Cost2Kern kern = nullptr;
-            const bool two = items > kCost2Threads;
-            // numDisparities 128 / 256: the pair count is a compile-time
-            // constant (unrolled pixel-cost loop, immediate LDS offsets)
-            const int ppc = !ctx->cost_fixed_pp ? 0 : l2.PP == 64 ? 64 : (l2.PP == 128 ? 128 : 0);
             if (ppc != 64) *Bv = nullptr;  // the bit-sliced plane: D = 128 kernels only
             kern = cost2_pick(2 * e.SH2 + 1, two ? 2 : 1, ppc);
-            if (l2.bytes > 65536 &&
+            if (lbytes > 65536 &&
                 (rc = check_hip(ctx, hipFuncSetAttribute((const void*)kern,
                                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                         (int)l2.bytes),
+                                                         (int)lbytes),
                                 "sgbm cost LDS attribute")))
                 return rc;
             {
                 StageTimer tm(ctx, kStageCost);
-                hipLaunchKernelGGL(kern, grid2, dim3(kCost2Threads), l2.bytes, s, pre, W, H, e, TY,
+                hipLaunchKernelGGL(kern, grid2, dim3(kCost2Threads), lbytes, s, pre, W, H, e, TY,
                                    Cv, *Bv ? nullptr : *Rv, Mv, *Bv, ctx->cost_xcd ? 1 : 0);
             }
             *pinned_hh = e.fullDP != 0;  // MODE_HH fix-up rows/column written by the kernel
