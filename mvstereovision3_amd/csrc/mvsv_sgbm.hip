@@ -562,9 +562,6 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                     const uint32_t c1 =
                         bt_cost2(pl4[2 * CLC * k + 1], pl2[2 * CLC * k + 1], qb4[CLC * k], qb2[CLC * k]);
                     pp[CLC * k] = make_uint2(c0, c1);
-#if MVSV_COST2_PIX_FENCE
-                    __builtin_amdgcn_sched_barrier(0);
-#endif
                 }
                 return;
             }
@@ -675,14 +672,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                 // subtracts a term the sum holds)
                 for (int q = 0; q < NR; q++) h = add2_nc(h, wv[q]);
                 const bool emit = k >= NR - 1;
-                // the step's row offsets from an opaque copy of k: otherwise the
-                // compiler keeps one set of output addresses per unrolled step
-                // live across the loop (registers the ring needs)
-                int ko = k;
-#if MVSV_COST2_OPAQUE_K
-                asm volatile("" : "+s"(ko));
-#endif
-                uint32_t* orow = obase + (size_t)ko * ostride;
+                uint32_t* orow = obase + (size_t)k * ostride;
                 // MODE_HH: OpenCV 3.4 leaves P2 in the rows it never recomputes
                 // (y >= H - SH2) and in column x = 0 of rows y >= 1
                 const int yo = y0 - 2 * SH2 + k;
@@ -772,7 +762,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                             // the four-pixel group of the wave's columns (mvsv_bitslice.hpp
                             // cq_word): word (q' = 2 h + e) * 16 + c * 4 + b
                             const int qw = (2 * (p >> 5) + ((q & 7) >> 2)) * 16 + c * 4 + (q & 3);
-                            if (full || c < nout) bq[(ptrdiff_t)ko * W1q * 16 + qw] = tw;
+                            if (full || c < nout) bq[(ptrdiff_t)k * W1q * 16 + qw] = tw;
                             // C is read only for the WTA's C(best -+ 1) gathers, so it
                             // is stored [frame][y][x / 4][d][x % 4] (rows padded to
                             // a multiple of 4 pixels, read by mvsv_bsgm.hip bsgm_wta_kernel):
@@ -781,7 +771,7 @@ __global__ __launch_bounds__(kCost2Threads) __attribute__((amdgpu_waves_per_eu(4
                             // wave's 1 KiB as one run
                             // (a wave wholly right of W1 -- nout <= 0 -- would land in
                             // the next row)
-                            if (nout > 0) cq[(ptrdiff_t)ko * W1q * 16] = make_uint4(Plo01, Plo23, Phi01, Phi23);
+                            if (nout > 0) cq[(ptrdiff_t)k * W1q * 16] = make_uint4(Plo01, Plo23, Phi01, Phi23);
                         }
                     }
                     if (Rv) {
