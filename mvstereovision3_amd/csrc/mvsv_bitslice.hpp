@@ -171,6 +171,55 @@ MVSV_BS_HD void add55(const uint32_t (&a)[5], const uint32_t (&b)[5], uint32_t (
     v[5] = lop3<kMaj>(a[4], b[4], k3);
 }
 
+// The WTA's S'' = n C' + (sum of the n deltas), 7 bits.
+// MODE_HH (n = 8): s6 = the eight deltas (<= 40), S'' = s6 + 8 C' <= 120 --
+// the low 3 bits of s6 stay, C' adds to the rest (7 instructions).
+MVSV_BS_HD void total8(const uint32_t (&c)[4], const uint32_t (&s6)[6], uint32_t (&S)[7])
+{
+    const uint32_t top[3] = {s6[3], s6[4], s6[5]};
+    uint32_t hi[4];
+    add43(c, top, hi);
+    S[0] = s6[0], S[1] = s6[1], S[2] = s6[2];
+    S[3] = hi[0], S[4] = hi[1], S[5] = hi[2], S[6] = hi[3];
+}
+// MODE_SGBM (n = 5): s5 = the five deltas (<= 25), S'' = (s5 + C') + 4 C' <= 75:
+// t = s5 + C' <= 35, its low 2 bits stay, C' adds to t >> 2 (<= 8; 17 instructions)
+MVSV_BS_HD void total5(const uint32_t (&c)[4], const uint32_t (&s5)[5], uint32_t (&S)[7])
+{
+    uint32_t t[6];
+    add54(s5, c, t);
+    const uint32_t a[4] = {t[2], t[3], t[4], t[5]};
+    uint32_t hi[5];
+    add44(a, c, hi);
+    S[0] = t[0], S[1] = t[1];
+    S[2] = hi[0], S[3] = hi[1], S[4] = hi[2], S[5] = hi[3], S[6] = hi[4];
+}
+
+// Tie rules of the WTA among the d that attain min S (d = 64 h + 2 p + e on
+// word bit p of parity e, half h): OpenCV 3.4's MODE_HH loop and later
+// releases take the smallest d; 3.4's MODE_SGBM SSE2 loop keeps one minimum
+// per SIMD lane d mod 8 (the first d of that lane) and takes the lowest lane
+// that holds the overall minimum -- the smallest (d mod 8, d).  Key of the
+// winner among the set bits `mask` of one word (smaller key wins; d in the low
+// 7 bits; 1 << 20 for an empty mask).  d mod 8 = 2 (p mod 4) + e.
+MVSV_BS_HD int wta_key(uint32_t mask, int h, int e, bool lane_rule)
+{
+    if (!mask) return 1 << 20;
+    uint32_t sel = mask;
+    if (lane_rule) {
+        const uint32_t m0 = mask & 0x11111111u, m1 = mask & 0x22222222u, m2 = mask & 0x44444444u;
+        sel = m0 ? m0 : m1 ? m1 : m2 ? m2 : mask;
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int p = __builtin_ctz(sel);
+#else
+    int p = 0;
+    while (!((sel >> p) & 1u)) p++;
+#endif
+    const int d = 64 * h + 2 * p + e;
+    return lane_rule ? ((2 * (p & 3) + e) << 7) | d : d;
+}
+
 // s = min(v - m, P2) for a 4-bit v >= m and a lane-uniform 3-bit m given as
 // all-ones / all-zero masks m0..m2 (13 instructions)
 template <int P2>

@@ -647,17 +647,20 @@ __device__ __forceinline__ void bs_dir_chains(const uint32_t* __restrict__ Bc, u
 }
 
 // blockIdx.z = pass * 3 + slot (slot 0, 1, 2: DX = +1, 0, -1); blockIdx.x: 16
-// chains, as many as the longest direction has (W1 + H - 1).  z = 6, 7: the two
-// line directions (16 rows per block) into planes 6 and 7 -- one launch for all
-// eight directions (a small launch pays no stream fork / join)
+// chains, as many as the longest direction has (W1 + H - 1).  z = 3 npass,
+// 3 npass + 1: the two line directions (16 rows per block) into the planes
+// after the vertical / diagonal ones -- one launch for all eight (MODE_HH,
+// npass 2) or five (MODE_SGBM, npass 1) directions (a small launch pays no
+// stream fork / join)
 template <int P1, int P2>
 __global__ __launch_bounds__(64) void bsgm_dir_kernel(const uint32_t* __restrict__ Bc, uint32_t* __restrict__ Dp,
                                                        size_t plane_words, int H, int W1,
-                                                       uint32_t* __restrict__ dummy)
+                                                       uint32_t* __restrict__ dummy, int npass)
 {
-    if (blockIdx.z >= 6) {
+    const int zl = 3 * npass;
+    if ((int)blockIdx.z >= zl) {
         if ((int)blockIdx.x * 16 < H)
-            bs_line_chains<P1, P2>(Bc, Dp + 6 * plane_words, plane_words, H, W1, blockIdx.z == 7);
+            bs_line_chains<P1, P2>(Bc, Dp + (size_t)zl * plane_words, plane_words, H, W1, (int)blockIdx.z > zl);
         return;
     }
     const int pass = blockIdx.z / 3, slot = blockIdx.z - 3 * pass;
@@ -681,15 +684,16 @@ __global__ __launch_bounds__(64) void bsgm_dir_kernel(const uint32_t* __restrict
 // S(best -+ 1) from S'' and, where the residual may be clamped, the C gathers;
 // the parabola, the raw map, the right-view key.  best / mins / Sm / Sp: argmin,
 // minimum S'' and S''(best -+ 1) of pixel pix (cost column x of its row).
-constexpr int kBsNdir = 8;
+// ndir = 8 (MODE_HH) or 5 (MODE_SGBM) directions: S = n (C - P2) + sum of deltas
 __device__ __forceinline__ void bs_finish_pixel(const int16_t* __restrict__ C, const uint16_t* __restrict__ Mv,
                                                 size_t pix, int W1, int W, int x, int best, int mins, int Sm,
                                                 int Sp, const SgbmEff& e, int16_t* orow, uint32_t* krow)
 {
     const int D = e.D;
-    const int clampS = kBsNdir * 2 * e.P2;  // S'' >= this: C'' may be the clamp value
+    const int ndir = e.fullDP ? 8 : 5;
+    const int clampS = ndir * 2 * e.P2;  // S'' >= this: C'' may be the clamp value
     const int mC = Mv[pix];
-    const int base = kBsNdir * (mC - e.P2);  // S = min(base + S', MAX_COST)
+    const int base = ndir * (mC - e.P2);  // S = min(base + S', MAX_COST)
     const int bm = max(best - 1, 0), bp = min(best + 1, D - 1);
     const bool need = Sm >= clampS || Sp >= clampS;
     // C is stored [frame][y][x / 4][d][x % 4] on this pipeline (the cost
@@ -699,7 +703,7 @@ __device__ __forceinline__ void bs_finish_pixel(const int16_t* __restrict__ C, c
     auto cword = [&](int d) -> int { return need ? (int)(uint16_t)C[cbase + d * 4] : 0; };
     auto exact = [&](int Spp, int cv) -> int {
         const int c1 = Spp >= clampS ? cv - mC : 0;
-        return min(base + Spp + kBsNdir * (c1 - min(c1, 2 * e.P2)), kMaxCost);
+        return min(base + Spp + ndir * (c1 - min(c1, 2 * e.P2)), kMaxCost);
     };
     const int minS = min(base + mins, kMaxCost);
     const int Smx = exact(Sm, cword(bm)), Spx = exact(Sp, cword(bp));
@@ -740,7 +744,11 @@ __device__ __forceinline__ void bs_lr_check_row(int16_t* orow, const uint32_t* k
 
 constexpr int kBsWtaThreads = 512;
 
-template <bool SIDE>
+// NDIR = 8 (MODE_HH) / 5 (MODE_SGBM: the down pass's three directions and the
+// two row directions).  SIDE: NDIR grouped delta planes (the side-by-side
+// directions, then the two row directions); otherwise the strip passes' 4-bit
+// planes (NDIR / 4 of them) and the two line planes.
+template <bool SIDE, int NDIR>
 __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t* __restrict__ Bc,
                                                                  const uint32_t* __restrict__ A, size_t aplane,
                                                                  const uint32_t* __restrict__ Dl, size_t dplane,
@@ -749,9 +757,11 @@ __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t*
                                                                  SgbmEff e, int16_t* __restrict__ raw,
                                                                  uint32_t* __restrict__ keys)
 {
+    static_assert(NDIR == 8 || NDIR == 5, "8 or 5 directions");
     const int y = blockIdx.x, f = blockIdx.y;
     const int W1 = e.W1;
     const int INV = e.invalid;
+    const bool lane_rule = NDIR == 5 && !(e.variant & MVSV_VARIANT_WTA_MIN_D);
     int16_t* orow = raw + ((size_t)f * H + y) * W;
     uint32_t* krow = keys + ((size_t)f * H + y) * W;
     for (int x = threadIdx.x; x < W; x += kBsWtaThreads) {
@@ -767,75 +777,83 @@ __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t*
         const bool own = xr < W1;
         const int x = min(xr, W1 - 1);
         const size_t pix = pix0 + x;
-        uint32_t c[2][4], ad[2][4], au[2][4], dl[2][3], dr[2][3];
+        uint32_t c[2][4];
         uint32_t S[2][7];
+        const size_t rowq = (size_t)(f * H + y) * bs::padq(W1);
+        const uint32_t* qc = Bc + bs::cq_word(rowq, x, 2 * h);
         if constexpr (SIDE) {
-            // eight grouped delta planes (six side-by-side directions, then the
-            // two line directions): S'' = 8 C' + the eight deltas
-            const size_t rowq = (size_t)(f * H + y) * bs::padq(W1);
-            const uint32_t* qc = Bc + bs::cq_word(rowq, x, 2 * h);
+            // NDIR grouped delta planes: S'' = NDIR C' + the deltas
 #pragma unroll
             for (int e2 = 0; e2 < 2; e2++) {
                 const uint4 t = *(const uint4*)(qc + 16 * e2);
                 c[e2][0] = t.x, c[e2][1] = t.y, c[e2][2] = t.z, c[e2][3] = t.w;
-                uint32_t dd[8][3];
+                uint32_t dd[NDIR][3];
 #pragma unroll
-                for (int i = 0; i < 8; i++) {
+                for (int i = 0; i < NDIR; i++) {
                     const uint32_t* qd = Dl + (size_t)i * dplane + bs::dl_word(rowq, x, 2 * h + e2);
 #pragma unroll
                     for (int b = 0; b < 3; b++) dd[i][b] = qd[b];
                 }
-                uint32_t a4[4][4], a5[2][5], s6[6], hi[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) bs::add33(dd[2 * i], dd[2 * i + 1], a4[i]);
-                bs::add44(a4[0], a4[1], a5[0]);
-                bs::add44(a4[2], a4[3], a5[1]);
-                bs::add55(a5[0], a5[1], s6);  // all deltas <= 8 P2 = 40
-                const uint32_t top[3] = {s6[3], s6[4], s6[5]};
-                bs::add43(c[e2], top, hi);
-                S[e2][0] = s6[0], S[e2][1] = s6[1], S[e2][2] = s6[2];
-                S[e2][3] = hi[0], S[e2][4] = hi[1], S[e2][5] = hi[2], S[e2][6] = hi[3];
+                uint32_t a4[4][4], a5[2][5], s6[6];
+                bs::add33(dd[0], dd[1], a4[0]);
+                bs::add33(dd[2], dd[3], a4[1]);
+                bs::add44(a4[0], a4[1], a5[0]);  // <= 4 P2
+                if constexpr (NDIR == 8) {
+                    bs::add33(dd[4], dd[5], a4[2]);
+                    bs::add33(dd[6], dd[7], a4[3]);
+                    bs::add44(a4[2], a4[3], a5[1]);
+                    bs::add55(a5[0], a5[1], s6);  // all deltas <= 8 P2 = 40
+                    bs::total8(c[e2], s6, S[e2]);
+                } else {
+                    const uint32_t d4[4] = {dd[4][0], dd[4][1], dd[4][2], 0u};
+                    bs::add54(a5[0], d4, s6);  // all deltas <= 5 P2 = 25 (bit 5 zero)
+                    const uint32_t s5[5] = {s6[0], s6[1], s6[2], s6[3], s6[4]};
+                    bs::total5(c[e2], s5, S[e2]);
+                }
             }
         } else {
-            // grouped C' and line planes (bs::cq_word / dl_word), E then O
-            const size_t rowq = (size_t)(f * H + y) * bs::padq(W1);
-            const uint32_t* qc = Bc + bs::cq_word(rowq, x, 2 * h);
+            // grouped C' and line planes (bs::cq_word / dl_word), E then O; the
+            // strip planes per pixel (word h * 8 + e * 4 + b)
             const uint4* qd = (const uint4*)(A + pix * 16 + h * 8);
             const uint4* qu = (const uint4*)(A + aplane + pix * 16 + h * 8);
             const uint32_t* ql = Dl + bs::dl_word(rowq, x, 2 * h);
             const uint32_t* qr = Dl + dplane + bs::dl_word(rowq, x, 2 * h);
-            uint4 t;
 #pragma unroll
             for (int e2 = 0; e2 < 2; e2++) {
-                t = *(const uint4*)(qc + 16 * e2);
+                uint4 t = *(const uint4*)(qc + 16 * e2);
                 c[e2][0] = t.x, c[e2][1] = t.y, c[e2][2] = t.z, c[e2][3] = t.w;
+                uint32_t ad[4], dl[3], dr[3];
                 t = qd[e2];
-                ad[e2][0] = t.x, ad[e2][1] = t.y, ad[e2][2] = t.z, ad[e2][3] = t.w;
-                t = qu[e2];
-                au[e2][0] = t.x, au[e2][1] = t.y, au[e2][2] = t.z, au[e2][3] = t.w;
+                ad[0] = t.x, ad[1] = t.y, ad[2] = t.z, ad[3] = t.w;
 #pragma unroll
                 for (int b = 0; b < 3; b++) {
-                    dl[e2][b] = ql[12 * e2 + b];
-                    dr[e2][b] = qr[12 * e2 + b];
+                    dl[b] = ql[12 * e2 + b];
+                    dr[b] = qr[12 * e2 + b];
+                }
+                uint32_t d4[4];
+                bs::add33(dl, dr, d4);  // lines <= 2 P2 = 10
+                if constexpr (NDIR == 8) {
+                    uint32_t au[4], s5[5], s6[6];
+                    t = qu[e2];
+                    au[0] = t.x, au[1] = t.y, au[2] = t.z, au[3] = t.w;
+                    bs::add44(ad, au, s5);  // strips <= 2 * 3 P2 = 30
+                    bs::add54(s5, d4, s6);  // all deltas <= 8 P2 = 40
+                    bs::total8(c[e2], s6, S[e2]);
+                } else {
+                    uint32_t s5[5];
+                    bs::add44(ad, d4, s5);  // all deltas <= 5 P2 = 25
+                    bs::total5(c[e2], s5, S[e2]);
                 }
             }
-#pragma unroll
-            for (int e2 = 0; e2 < 2; e2++) {
-                uint32_t s5[5], d4[4], s6[6], hi[4];
-                bs::add44(ad[e2], au[e2], s5);  // strips <= 2 * 3 P2 = 30
-                bs::add33(dl[e2], dr[e2], d4);  // lines <= 2 P2 = 10
-                bs::add54(s5, d4, s6);          // all deltas <= 8 P2 = 40
-                const uint32_t top[3] = {s6[3], s6[4], s6[5]};
-                bs::add43(c[e2], top, hi);      // 8 C' + deltas: high part <= 10 + 5
-                S[e2][0] = s6[0], S[e2][1] = s6[1], S[e2][2] = s6[2];
-                S[e2][3] = hi[0], S[e2][4] = hi[1], S[e2][5] = hi[2], S[e2][6] = hi[3];
-            }
         }
-        // argmin: the minimum is <= 8 P2 = 40 < 64 (the d with C' = 0), so bit 6 is 0
-        uint32_t kE = ~S[0][6], kO = ~S[1][6];
+        // argmin: the minimum is <= NDIR P2 (the d with C' = 0): < 64 (bit 6
+        // zero) for 8 directions, < 32 (bits 5, 6 zero) for 5
+        constexpr int TOP = NDIR == 8 ? 5 : 4;
+        uint32_t kE = NDIR == 8 ? ~S[0][6] : ~(S[0][6] | S[0][5]);
+        uint32_t kO = NDIR == 8 ? ~S[1][6] : ~(S[1][6] | S[1][5]);
         int mins = 0;
 #pragma unroll
-        for (int b = 5; b >= 0; b--) {
+        for (int b = TOP; b >= 0; b--) {
             const uint32_t zE = bs::lop3<bs::kAndNotAB>(S[0][b], kE, kE);
             const uint32_t zO = bs::lop3<bs::kAndNotAB>(S[1][b], kO, kO);
             uint32_t any = zE | zO;
@@ -845,12 +863,11 @@ __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t*
             kO = fz ? zO : kO;
             mins |= fz ? 0 : 1 << b;
         }
-        // smallest d among the minima: the lower lane first, then the lowest bit
-        // position, even before odd
-        const uint32_t m = kE | kO;
-        const int p = __builtin_ctz(m | 0x80000000u);
-        const int mine = m ? 64 * h + 2 * p + (((kE >> p) & 1u) ? 0 : 1) : 1 << 20;
-        const int best = min(mine, (int)xswap((uint32_t)mine));
+        // the tie rule among the minima (bs::wta_key): both parities of the
+        // lane, then the partner lane
+        int key = min(bs::wta_key(kE, h, 0, lane_rule), bs::wta_key(kO, h, 1, lane_rule));
+        key = min(key, (int)xswap((uint32_t)key));
+        const int best = key & 127;
         // S''(best -+ 1): both have the other parity; each lane reads its half
         const int eb = best & 1;
         int Sm = 0, Sp = 0;
@@ -886,12 +903,15 @@ __global__ __launch_bounds__(kBsWtaThreads) void bsgm_wta_kernel(const uint32_t*
 // ---------------------------------------------------------------------------
 constexpr int kBsRG = 3;  // groups (12 steps) of operands in the register ring
 
-template <int P1, int P2>
+// NDIR = 8 (MODE_HH: both strip passes' planes) or 5 (MODE_SGBM: the down pass
+// only); lane_rule: MODE_SGBM's lane tie rule (bs::wta_key)
+template <int P1, int P2, int NDIR>
 __global__ __launch_bounds__(64) void bsgm_rlwta_kernel(const uint32_t* __restrict__ Bc,
                                                          const uint32_t* __restrict__ A, size_t aplane,
                                                          const uint32_t* __restrict__ Dlr, int H, int W1,
-                                                         uint32_t* __restrict__ rec)
+                                                         uint32_t* __restrict__ rec, int lane_rule)
 {
+    static_assert(NDIR == 8 || NDIR == 5, "8 or 5 directions");
     const int lane = threadIdx.x;
     const int q = lane & 3, rr = lane >> 2;
     const int y = min((int)blockIdx.x * 16 + rr, H - 1);
@@ -923,7 +943,7 @@ __global__ __launch_bounds__(64) void bsgm_rlwta_kernel(const uint32_t* __restri
         for (int u = 0; u < 4; u++) {
             const int x = min(4 * g + u, W1 - 1);
             o.a[u] = adn[(size_t)x * 4];
-            o.b[u] = aup[(size_t)x * 4];
+            if constexpr (NDIR == 8) o.b[u] = aup[(size_t)x * 4];
         }
     };
     const int ph = part ? 1 : 0;
@@ -949,22 +969,29 @@ __global__ __launch_bounds__(64) void bsgm_rlwta_kernel(const uint32_t* __restri
                 for (int b = 0; b < 3; b++) st[b] = nw[b];
                 // S'' of this lane's 32 disparities
                 const uint32_t ad[4] = {o.a[u].x, o.a[u].y, o.a[u].z, o.a[u].w};
-                const uint32_t au[4] = {o.b[u].x, o.b[u].y, o.b[u].z, o.b[u].w};
                 uint32_t dl[3];
 #pragma unroll
                 for (int b = 0; b < 3; b++) dl[b] = w4(o.d[(3 * u + b) >> 2], (3 * u + b) & 3);
-                uint32_t s5[5], d4[4], s6[6], hi[4];
-                bs::add44(ad, au, s5);  // strips <= 2 * 3 P2 = 30
+                uint32_t d4[4], S[7];
                 bs::add33(dl, dr, d4);  // lines <= 2 P2 = 10
-                bs::add54(s5, d4, s6);  // all deltas <= 8 P2 = 40
-                const uint32_t top[3] = {s6[3], s6[4], s6[5]};
-                bs::add43(cw, top, hi);  // + 8 C'
-                const uint32_t S[7] = {s6[0], s6[1], s6[2], hi[0], hi[1], hi[2], hi[3]};
-                // argmin over the quad: the minimum is <= 8 P2 = 40 < 64, bit 6 is 0
-                uint32_t kk = ~S[6];
+                if constexpr (NDIR == 8) {
+                    const uint32_t au[4] = {o.b[u].x, o.b[u].y, o.b[u].z, o.b[u].w};
+                    uint32_t s5[5], s6[6];
+                    bs::add44(ad, au, s5);  // strips <= 2 * 3 P2 = 30
+                    bs::add54(s5, d4, s6);  // all deltas <= 8 P2 = 40
+                    bs::total8(cw, s6, S);  // + 8 C'
+                } else {
+                    uint32_t s5[5];
+                    bs::add44(ad, d4, s5);  // all deltas <= 5 P2 = 25
+                    bs::total5(cw, s5, S);  // + 5 C'
+                }
+                // argmin over the quad: the minimum is <= NDIR P2, below 64 (8
+                // directions: bit 6 zero) / 32 (5: bits 5 and 6 zero)
+                constexpr int TOP = NDIR == 8 ? 5 : 4;
+                uint32_t kk = NDIR == 8 ? ~S[6] : ~(S[6] | S[5]);
                 int mins = 0;
 #pragma unroll
-                for (int b = 5; b >= 0; b--) {
+                for (int b = TOP; b >= 0; b--) {
                     const uint32_t z = bs::lop3<bs::kAndNotAB>(S[b], kk, kk);
                     uint32_t any = z | xswap(z);
                     any |= (uint32_t)__builtin_amdgcn_mov_dpp((int)any, 0x4E, 0xf, 0xf, true);
@@ -972,10 +999,11 @@ __global__ __launch_bounds__(64) void bsgm_rlwta_kernel(const uint32_t* __restri
                     kk = fz ? z : kk;
                     mins |= fz ? 0 : 1 << b;
                 }
-                // smallest d among the minima (d = 64 h + 2 p + e)
-                int best = kk ? 64 * h + 2 * __builtin_ctz(kk) + eo : 1 << 20;
-                best = min(best, (int)xswap((uint32_t)best));
-                best = min(best, __builtin_amdgcn_mov_dpp(best, 0x4E, 0xf, 0xf, true));
+                // the tie rule among the minima (bs::wta_key; d = 64 h + 2 p + e)
+                int key = bs::wta_key(kk, h, eo, NDIR == 5 && lane_rule);
+                key = min(key, (int)xswap((uint32_t)key));
+                key = min(key, __builtin_amdgcn_mov_dpp(key, 0x4E, 0xf, 0xf, true));
+                const int best = key & 127;
                 // S''(best -+ 1) from the lane that holds it
                 auto sat = [&](int d) -> uint32_t {
                     const int dq = 2 * ((d >> 6) & 1) + (d & 1), p = ((d & 63) >> 1);
@@ -1042,6 +1070,50 @@ __global__ __launch_bounds__(kBsFinThreads) void bsgm_rl_final_kernel(const uint
     bs_lr_check_row(orow, krow, W, e, kBsFinThreads);
 }
 
+// ---------------------------------------------------------------------------
+// MODE_SGBM's cost-row quirks on the bit-sliced layouts (OpenCV 3.4, SURVEY
+// Appendix A.3; the int16 form is sgbm_cost_fixup_*_kernel in mvsv_sgbm.hip):
+// rows y >= ybot = H - SH2 are never recomputed and keep row ylast, and
+// (without MVSV_VARIANT_FIRSTCOL_FIX) column 0 of every row y >= 1 keeps C(0, 0).
+// A pixel's C' words, its pixel-quad C and its minimum m move together.  MODE_HH
+// pins those cells to P2 inside the cost kernel instead.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bsgm_fixup_bottom_kernel(uint32_t* __restrict__ Bc, int16_t* __restrict__ C,
+                                                                uint16_t* __restrict__ Mv, int H, int W1, int ylast,
+                                                                int ybot)
+{
+    const int y = ybot + blockIdx.y, f = blockIdx.z;
+    const size_t W1q = (size_t)bs::padq(W1);
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t nb = W1q * 4, nc = W1q * 16;  // uint4 per row: C' (64 B / pixel), C (256 B / pixel)
+    const size_t src = (size_t)f * H + ylast, dst = (size_t)f * H + y;
+    if (i < nb) {
+        ((uint4*)Bc)[dst * nb + i] = ((const uint4*)Bc)[src * nb + i];
+    } else if (i < nb + nc) {
+        const size_t j = i - nb;
+        ((uint4*)C)[dst * nc + j] = ((const uint4*)C)[src * nc + j];
+    }
+    if (i < (size_t)W1) Mv[dst * W1 + i] = Mv[src * W1 + i];
+}
+
+// column 0 of rows 1 .. H - 1 <- pixel (0, 0) of the frame (D = 128)
+__global__ __launch_bounds__(128) void bsgm_fixup_col0_kernel(uint32_t* __restrict__ Bc, int16_t* __restrict__ C,
+                                                              uint16_t* __restrict__ Mv, int H, int W1)
+{
+    const int y = 1 + blockIdx.x, f = blockIdx.y;
+    const size_t W1q = (size_t)bs::padq(W1);
+    const size_t r0 = (size_t)f * H, r = r0 + y;
+    const int t = threadIdx.x;
+    if (t < 16) {
+        // word (q, b) of pixel 0 in its group: q * 16 + b (bs::cq_word)
+        const int o = (t >> 2) * 16 + (t & 3);
+        Bc[bs::cq_word(r * W1q, 0, 0) + o] = Bc[bs::cq_word(r0 * W1q, 0, 0) + o];
+    }
+    // pixel-quad C: [row][x / 4][d][x % 4]
+    C[(r * W1q) * 128 + t * 4] = C[(r0 * W1q) * 128 + t * 4];
+    if (t == 0) Mv[r * W1] = Mv[r0 * W1];
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1051,7 +1123,7 @@ bool bsgm_eligible(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H)
 {
     const long bs = 2L * e.SW2 + 1;
     const bool no_wrap = (long)e.P2 + bs * bs * (2L * e.ftzero + 63) + e.P2 <= 32767;
-    return ctx->bitslice && e.fullDP && e.D == 128 && e.P1 == 2 && e.P2 == 5 && e.uniq == 0 && no_wrap &&
+    return ctx->bitslice && e.D == 128 && e.P1 == 2 && e.P2 == 5 && e.uniq == 0 && no_wrap &&
            e.W1 > 0 && (size_t)n * H * bs::padq(e.W1) * 16 < ((size_t)1 << 31);
 }
 
@@ -1062,7 +1134,7 @@ static int launch_bs_strips(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const
                             size_t aplane, uint32_t* dummy)
 {
     using Cfg = BsStripCfg<NG>;
-    constexpr int npass = 2;
+    const int npass = e.fullDP ? 2 : 1;  // MODE_SGBM: the down pass only
     const int nstrips = (e.W1 + H - 1 + Cfg::kSW - 1) / Cfg::kSW;
     const size_t bytes = (size_t)npass * n * nstrips * H * kBsGran * 8;
     int rc;
@@ -1136,22 +1208,44 @@ static int bsgm_paths_side(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e,
                            const uint32_t* Bv, const uint16_t* Mv, int16_t* raw)
 {
     int rc;
+    const int npass = e.fullDP ? 2 : 1, ndir = 3 * npass + 2;
     const size_t dplane = (size_t)n * H * bs::padq(e.W1) * 12;  // words per delta plane (grouped)
     // + 256 words: dummy store slots of cells outside the image
-    if ((rc = ensure(ctx, ctx->agg, (8 * dplane + 256) * 4, "bit-sliced delta planes"))) return rc;
+    if ((rc = ensure(ctx, ctx->agg, (ndir * dplane + 256) * 4, "bit-sliced delta planes"))) return rc;
     if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
     uint32_t* Dv = (uint32_t*)ctx->agg.ptr;
     hipStream_t s = ctx->stream;
     {
         StageTimer tm(ctx, kStagePath);
-        hipLaunchKernelGGL((bsgm_dir_kernel<2, 5>), dim3((e.W1 + H - 1 + 15) / 16, n, 8), dim3(64), 0, s, Bv, Dv,
-                           dplane, H, e.W1, Dv + 8 * dplane);
+        hipLaunchKernelGGL((bsgm_dir_kernel<2, 5>), dim3((e.W1 + H - 1 + 15) / 16, n, ndir), dim3(64), 0, s, Bv,
+                           Dv, dplane, H, e.W1, Dv + ndir * dplane, npass);
         if ((rc = check_hip(ctx, hipGetLastError(), "bit-sliced direction kernel"))) return rc;
     }
     StageTimer tm(ctx, kStageFinal);
-    hipLaunchKernelGGL(bsgm_wta_kernel<true>, dim3(H, n), dim3(kBsWtaThreads), 0, s, Bv, nullptr, (size_t)0, Dv,
-                       dplane, Cv, Mv, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
+    if (e.fullDP)
+        hipLaunchKernelGGL((bsgm_wta_kernel<true, 8>), dim3(H, n), dim3(kBsWtaThreads), 0, s, Bv, nullptr, (size_t)0,
+                           Dv, dplane, Cv, Mv, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
+    else
+        hipLaunchKernelGGL((bsgm_wta_kernel<true, 5>), dim3(H, n), dim3(kBsWtaThreads), 0, s, Bv, nullptr, (size_t)0,
+                           Dv, dplane, Cv, Mv, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
     return check_hip(ctx, hipGetLastError(), "bit-sliced WTA kernel");
+}
+
+int bsgm_cost_fixup(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, uint32_t* Bv, uint16_t* Mv)
+{
+    if (e.fullDP || H <= 1) return MVSV_OK;  // MODE_HH: pinned inside the cost kernel
+    hipStream_t s = ctx->stream;
+    const int ybot = std::max(H - e.SH2, 1), ylast = std::max(H - e.SH2 - 1, 0);
+    StageTimer tm(ctx, kStageFixup);
+    if (ybot < H) {
+        const size_t items = (size_t)bs::padq(e.W1) * 20;  // uint4 of C' and C per row
+        hipLaunchKernelGGL(bsgm_fixup_bottom_kernel, dim3((unsigned)((items + 255) / 256), H - ybot, n), dim3(256),
+                           0, s, Bv, Cv, Mv, H, e.W1, ylast, ybot);
+    }
+    // after the bottom rows: their column 0 is C(0, 0) too (unless FIRSTCOL_FIX)
+    if (!(e.variant & MVSV_VARIANT_FIRSTCOL_FIX))
+        hipLaunchKernelGGL(bsgm_fixup_col0_kernel, dim3(H - 1, n), dim3(128), 0, s, Bv, Cv, Mv, H, e.W1);
+    return check_hip(ctx, hipGetLastError(), "bit-sliced cost fixup");
 }
 
 int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv, const uint32_t* Bv,
@@ -1159,13 +1253,15 @@ int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16
 {
     int rc;
     if (side) return bsgm_paths_side(ctx, n, H, W, e, Cv, Bv, Mv, raw);
+    const int npass = e.fullDP ? 2 : 1;  // strip passes (MODE_SGBM: down only)
     const size_t aplane = (size_t)n * H * e.W1 * 16;  // words per strip-pass plane
     const size_t dplane = (size_t)n * H * bs::padq(e.W1) * 12;  // words per line plane (grouped, padded rows)
     // + 512 words: the strip kernel's dummy store slots (cells outside the image)
-    if ((rc = ensure(ctx, ctx->agg, (2 * aplane + 2 * dplane + 512) * 4, "bit-sliced delta planes"))) return rc;
+    if ((rc = ensure(ctx, ctx->agg, (npass * aplane + 2 * dplane + 512) * 4, "bit-sliced delta planes")))
+        return rc;
     if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
     uint32_t* Av = (uint32_t*)ctx->agg.ptr;
-    uint32_t* Dv = Av + 2 * aplane;
+    uint32_t* Dv = Av + npass * aplane;
     hipStream_t s = ctx->stream;
     if (!ctx->aux) {
         if ((rc = check_hip(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking), "aux stream")) ||
@@ -1213,15 +1309,24 @@ int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16
     if (ctx->bs_fuse) {
         // per-pixel records in the (unused) R->L plane's space
         uint32_t* rec = Dv + dplane;
-        hipLaunchKernelGGL((bsgm_rlwta_kernel<2, 5>), dim3((H + 15) / 16, n), dim3(64), 0, s, Bv, Av, aplane, Dv,
-                           H, e.W1, rec);
+        const int lane_rule = !(e.variant & MVSV_VARIANT_WTA_MIN_D);
+        if (e.fullDP)
+            hipLaunchKernelGGL((bsgm_rlwta_kernel<2, 5, 8>), dim3((H + 15) / 16, n), dim3(64), 0, s, Bv, Av, aplane,
+                               Dv, H, e.W1, rec, lane_rule);
+        else
+            hipLaunchKernelGGL((bsgm_rlwta_kernel<2, 5, 5>), dim3((H + 15) / 16, n), dim3(64), 0, s, Bv, Av, aplane,
+                               Dv, H, e.W1, rec, lane_rule);
         if ((rc = check_hip(ctx, hipGetLastError(), "bit-sliced R->L + WTA kernel"))) return rc;
         hipLaunchKernelGGL(bsgm_rl_final_kernel, dim3(H, n), dim3(kBsFinThreads), 0, s, rec, Cv, Mv, H, W, e, raw,
                            (uint32_t*)ctx->keys.ptr);
         return check_hip(ctx, hipGetLastError(), "bit-sliced final kernel");
     }
-    hipLaunchKernelGGL(bsgm_wta_kernel<false>, dim3(H, n), dim3(kBsWtaThreads), 0, s, Bv, Av, aplane, Dv, dplane, Cv, Mv, H,
-                       W, e, raw, (uint32_t*)ctx->keys.ptr);
+    if (e.fullDP)
+        hipLaunchKernelGGL((bsgm_wta_kernel<false, 8>), dim3(H, n), dim3(kBsWtaThreads), 0, s, Bv, Av, aplane, Dv,
+                           dplane, Cv, Mv, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
+    else
+        hipLaunchKernelGGL((bsgm_wta_kernel<false, 5>), dim3(H, n), dim3(kBsWtaThreads), 0, s, Bv, Av, aplane, Dv,
+                           dplane, Cv, Mv, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
     return check_hip(ctx, hipGetLastError(), "bit-sliced WTA kernel");
 }
 

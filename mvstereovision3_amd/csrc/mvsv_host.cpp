@@ -483,7 +483,7 @@ size_t mvsv_sgbm_workspace_bytes(int n, int W, int H, const mvsv_sgbm_params* p)
     // (eight 48-byte planes side by side for small launches), strip boundary
     // granules (2 passes x strips of 64 U-columns x H rows x 36 u64)
     const long bsz = 2L * e.SW2 + 1;
-    const bool bs_regime = e.fullDP && e.D == 128 && e.P1 == 2 && e.P2 == 5 && e.uniq == 0 && e.W1 > 0 &&
+    const bool bs_regime = e.D == 128 && e.P1 == 2 && e.P2 == 5 && e.uniq == 0 && e.W1 > 0 &&
                            (long)e.P2 + bsz * bsz * (2L * e.ftzero + 63) + e.P2 <= 32767;
     if (bs_regime) {
         const size_t W1q = (size_t)(e.W1 + 3) & ~(size_t)3;

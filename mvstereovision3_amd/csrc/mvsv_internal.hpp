@@ -195,13 +195,16 @@ int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, con
 // poison != nullptr: when *poison == epoch (the launch `epoch` gave up a strip
 // wait) every output pixel is `invalid` instead of the median -- no map computed
 // from stale hand-off data leaves the pipeline.
-// Bit-sliced MODE_HH path aggregation + WTA (mvsv_bsgm.hip).  bsgm_eligible:
+// Bit-sliced path aggregation + WTA, MODE_HH and MODE_SGBM (mvsv_bsgm.hip).  bsgm_eligible:
 // the parameters admit it; the cost kernel then writes the C' planes Bv
 // (bsgm_plane_bytes) and bsgm_paths computes raw disparities from them.
 bool bsgm_eligible(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H);
 size_t bsgm_plane_bytes(int n, int H, int W1);
 int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv, const uint32_t* Bv,
                const uint16_t* Mv, int16_t* raw, bool side);
+// MODE_SGBM's never-recomputed rows and column 0 on the bit-sliced layouts (C'
+// planes, pixel-quad C, m); no-op for MODE_HH, whose cost kernel pins them
+int bsgm_cost_fixup(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, uint32_t* Bv, uint16_t* Mv);
 int median3x3_device(mvsv_ctx* ctx, int n, const int16_t* src, size_t ss, size_t sfs,
                      int16_t* dst, size_t ds, size_t dfs, int W, int H,
                      const int* poison = nullptr, unsigned epoch = 0, int invalid = 0);

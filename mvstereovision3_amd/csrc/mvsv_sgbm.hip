@@ -3410,7 +3410,11 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
 
     const int ybot = std::max(H - e.SH2, 1);     // first row that is never recomputed
     const int ylast = std::max(H - e.SH2 - 1, 0);  // last recomputed row
-    if (H > 1 && !pinned_hh) {
+    if (Bv) {
+        // bit-sliced layouts (MODE_SGBM: copied rows / column 0; MODE_HH: pinned
+        // by the cost kernel)
+        if ((rc = bsgm_cost_fixup(ctx, n, H, e, Cv, Bv, Mv))) return rc;
+    } else if (H > 1 && !pinned_hh) {
         StageTimer tm(ctx, kStageFixup);
         // OpenCV 3.4 quirks: rows >= 1 never refresh column 0; rows with
         // y + SH2 >= H are never recomputed (MODE_SGBM keeps the last computed

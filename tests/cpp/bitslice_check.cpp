@@ -112,6 +112,45 @@ static void check_helpers(std::mt19937& rng)
     sc(std::integral_constant<int, 3>());
     sc(std::integral_constant<int, 4>());
     sc(std::integral_constant<int, 5>());
+
+    // the WTA totals: S'' = 8 C' + s (s <= 40) and 5 C' + s (s <= 25)
+    for (int it = 0; it < 2000; it++) {
+        uint32_t c[4] = {0, 0, 0, 0}, s6[6] = {0, 0, 0, 0, 0, 0}, s5[5] = {0, 0, 0, 0, 0}, S8[7], S5[7];
+        int vc[32], v8[32], v5[32];
+        for (int p = 0; p < 32; p++) {
+            vc[p] = rng() % (2 * P2 + 1);
+            v8[p] = rng() % (8 * P2 + 1);
+            v5[p] = rng() % (5 * P2 + 1);
+            put(c, p, vc[p]);
+            put(s6, p, v8[p]);
+            put(s5, p, v5[p]);
+        }
+        total8(c, s6, S8);
+        total5(c, s5, S5);
+        for (int p = 0; p < 32; p++) {
+            CHECK(bits_at<7>(S8, p) == 8 * vc[p] + v8[p], "total8");
+            CHECK(bits_at<7>(S5, p) == 5 * vc[p] + v5[p], "total5");
+        }
+    }
+    // wta_key: the smallest d, or the smallest (d mod 8, d) (MODE_SGBM lane rule)
+    for (int it = 0; it < 4000; it++) {
+        const uint32_t mask = it < 8 ? (1u << (rng() % 32)) : (uint32_t)rng() & (uint32_t)rng();
+        const int h = rng() % 2, e = rng() % 2;
+        int bd = -1, bl = -1;
+        for (int p = 0; p < 32; p++)
+            if ((mask >> p) & 1u) {
+                const int d = 64 * h + 2 * p + e;
+                if (bd < 0) bd = d;
+                if (bl < 0 || (d & 7) < (bl & 7)) bl = d;
+            }
+        const int k0 = wta_key(mask, h, e, false), k1 = wta_key(mask, h, e, true);
+        if (!mask) {
+            CHECK(k0 == (1 << 20) && k1 == (1 << 20), "wta_key empty");
+        } else {
+            CHECK(k0 == bd, "wta_key min d");
+            CHECK((k1 & 127) == bl && (k1 >> 7) == (bl & 7), "wta_key lane rule %08x", mask);
+        }
+    }
 }
 
 // One pixel's 128 disparities on two lanes (h = 0, 1), each with E / O words.
