@@ -195,8 +195,12 @@ def _summary(path, workload, sha, what):
 
 def kernel_source_sha() -> str:
     h = hashlib.sha256()
+    # the kernels and the host code that picks them (dispatch defaults, eligibility
+    # gates, launch shapes) and the ABI header: a summary goes stale when any changes
     for p in sorted(glob.glob(os.path.join(KERNEL_SOURCES, "*.hip")) +
-                    glob.glob(os.path.join(KERNEL_SOURCES, "*.hpp"))):
+                    glob.glob(os.path.join(KERNEL_SOURCES, "*.hpp")) +
+                    glob.glob(os.path.join(KERNEL_SOURCES, "*.cpp")) +
+                    [os.path.join(ROOT, "include", "mvsv.h")]):
         h.update(open(p, "rb").read())
     return h.hexdigest()[:16]
 
@@ -274,19 +278,24 @@ def config_table(mvsv, _lib, dev, steps=10, warmup=3):
             add(f"{name}_batch{n}", 640, 480, D, n, ms, ("bm", OPS_PER_PXD["bm"] * 640 * 480 * D * n),
                 pairs[0], out[0].cpu().numpy(), lambda L0, R0, bp=bp: pyoracle.bm(L0, R0, bp),
                 {"bm_match_kernel_ms": round(bm_ms / max(bm_n, 1), 4)})
-    # config 3: SGBM configs/sgbm.yml 640x480, one frame (the live-camera case), 5 and 8 paths
+    # config 3: SGBM configs/sgbm.yml 640x480, one frame (the live-camera case) and
+    # a batch of 8, 5 paths (mode 0: what sgbm.yml selects) and 8 paths; and the
+    # 5-path mode at the headline's 1280x960 batch of 8
     for mode in (0, 1):
         m = mvsv.StereoSGBM.create(0, 0, 0, 0, 0)
         assert mvsv.Disparity.loadSGBMParameters(os.path.join(cfg, "sgbm.yml"), m, mvsv.sgbmParameters())
         m.setMode(mode)
         p = {k: v for k, v in m.params().items() if k != "variant"}
-        pairs, L, R = frames(1, 640, 480, 1, 128)
-        out = torch.empty((1, 480, 640), dtype=torch.int16, device=dev)
-        ms = timed(lambda: m.compute(L, R, out))
-        roof = ("hbm", 4 * 640 * 480 * 129) if mode else ("sgbm5", OPS_PER_PXD["sgbm5"] * 640 * 480 * 128)
-        add(f"config3_sgbm_yml_640x480_{'8path' if mode else '5path'}_batch1", 640, 480, 128, 1, ms, roof,
-            pairs[0], out[0].cpu().numpy(), lambda L0, R0, p=p: pyoracle.sgbm(L0, R0, p),
-            {"mode": "MODE_HH" if mode else "MODE_SGBM"})
+        shapes = [(640, 480, 1), (640, 480, 8)] + ([(1280, 960, 8)] if mode == 0 else [])
+        for W, H, n in shapes:
+            pairs, L, R = frames(n, W, H, 1, 128)
+            out = torch.empty((n, H, W), dtype=torch.int16, device=dev)
+            ms = timed(lambda: m.compute(L, R, out))
+            roof = ("hbm", 4 * W * H * 129 * n) if mode else ("sgbm5", OPS_PER_PXD["sgbm5"] * W * H * 128 * n)
+            name = (f"config3_sgbm_yml_640x480_{'8path' if mode else '5path'}_batch{n}" if W == 640
+                    else f"sgbm_{W}x{H}_d128_5path_batch{n}")
+            add(name, W, H, 128, n, ms, roof, pairs[0], out[0].cpu().numpy(),
+                lambda L0, R0, p=p: pyoracle.sgbm(L0, R0, p), {"mode": "MODE_HH" if mode else "MODE_SGBM"})
     # config 5: liveDisparity's create(0, 256, 9, 648, 2592) (trgt/liveDisparity.cpp:61,
     # MODE_SGBM, no speckle) at 1280x960: one frame and the stream's batch of 8
     m256 = mvsv.StereoSGBM.create(0, 256, 9, 648, 2592)
@@ -298,6 +307,19 @@ def config_table(mvsv, _lib, dev, steps=10, warmup=3):
         add(f"config5_sgbm_1280x960_d256_batch{n}", 1280, 960, 256, n, ms,
             ("sgbm5", OPS_PER_PXD["sgbm5"] * 1280 * 960 * 256 * n), pairs[0], out[0].cpu().numpy(),
             (lambda L0, R0, p=p256: pyoracle.sgbm(L0, R0, p)) if n == 1 else None, {"mode": "MODE_SGBM"})
+    # config 5 as BASELINE states it: the sustained stream (host frames in, maps and
+    # the 81 MeanDisparityDetection means out, the detection post-pass on every
+    # frame; trgt/liveDisparity.cpp:61,82-101, src/MeanDisparityDetection.cpp:159-266)
+    from tools.bench_stream import stream_measure
+    sm = stream_measure(mvsv, frames=240, depth=24, batch=8, inflight=2, device_steps=5)
+    recs["config5_stream_1280x960_d256_fps"] = {
+        "width": 1280, "height": 960, "num_disparities": 256, "stream_fps": sm["stream_fps"],
+        "stream_ms_per_frame": sm["stream_ms_per_frame"], "frames": sm["frames"], "depth": sm["depth"],
+        "batch": sm["batch"], "inflight": sm["inflight"], "host_ms_per_frame": sm["host_ms_per_frame"],
+        "device_resident_ms_per_frame_with_mean_grid": sm["device_resident_ms_per_frame"],
+        "obstacle_tiles_found": sm["obstacle_tiles_found"],
+        "note": "DisparityStream: host frames in, int16 map + 81 tile means out (PCIe incl.), "
+                "MeanDisparityDetection build(MEAN_VALUE) + detectObstacles per frame, in the timing"}
     # parity: frame 0 of every config against the oracle (outside all timing; the
     # batch-8 config-5 line shares frame 0's seed with the batch-1 line, checked once)
     pyoracle.lib()

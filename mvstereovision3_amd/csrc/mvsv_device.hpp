@@ -97,6 +97,63 @@ __device__ __forceinline__ int wave_min_i32(int v)
     return min(min(a, b), min(c, d));
 }
 
+// packed unsigned 16-bit pairs (VOP3P v_pk_*_u16)
+__device__ __forceinline__ uint32_t pk_subsat_u16(uint32_t a, uint32_t b)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, a),
+                                                                      __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
+}
+
+// Two independent u16 minima over each 16-lane row (packed in one dword).
+__device__ __forceinline__ uint32_t row_min_u16x2(uint32_t v)
+{
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false));
+    v = pk_min_u16(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, false));
+    return v;
+}
+
+// ... over aligned segments of `lanes` = 16, 32 or 64 lanes (wave-uniform):
+// the row butterfly, then rows (0,1) / (2,3) joined by v_permlane16_swap and the
+// two halves by v_permlane32_swap; every lane of a segment gets its minima.
+__device__ __forceinline__ uint32_t seg_min_u16x2(uint32_t v, int lanes)
+{
+    v = row_min_u16x2(v);
+    if (lanes >= 32) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        v = pk_min_u16(sw[0], sw[1]);
+    }
+    if (lanes >= 64) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        v = pk_min_u16(sw[0], sw[1]);
+    }
+    return v;
+}
+
 template <typename T>
 __device__ __forceinline__ T clampi(T v, T lo, T hi)
 {

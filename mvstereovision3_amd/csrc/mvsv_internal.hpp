@@ -191,6 +191,15 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
 int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, const uint8_t* R,
               size_t rs, size_t rfs, int W, int H, const BmEff& e, int16_t* out, size_t os,
               size_t ofs);
+// SGBM stages 1-3 (mvsv_cost.hip): BT interval planes, the cost volume (the
+// register-ring kernel also writes the residual plane *Rv or the bit-sliced C'
+// planes *Bv where given and possible -- each is set to nullptr otherwise), and
+// OpenCV 3.4's cost-row quirks on the int16 volume.
+int launch_prefilter(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, const uint8_t* R, size_t rs,
+                     size_t rfs, int W, int H, int ftzero, uint64_t* pre);
+int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int TY, const uint64_t* pre, int16_t* Cv,
+                uint8_t** Rv, uint16_t* Mv, bool* pinned_hh, uint32_t** Bv);
+int launch_cost_fixup(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, int16_t* Cv, uint8_t* Rv, uint16_t* Mv);
 // Post filters shared by both matchers.
 // poison != nullptr: when *poison == epoch (the launch `epoch` gave up a strip
 // wait) every output pixel is `invalid` instead of the median -- no map computed

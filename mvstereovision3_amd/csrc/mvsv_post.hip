@@ -226,16 +226,15 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(int16_t* __restrict_
     for (int k = 0; k < 4; k++) {
         const int ly = ty + 8 * k, li = ly * kSpTile + tx;
         root[k] = lval[li] != kInvalid ? lfind(lpar, li) : -1;
-        // wave-aggregated count: lanes sharing a root add once
-        bool pending = root[k] >= 0;
-        for (;;) {
-            unsigned long long m = __ballot(pending);
-            if (m == 0ull) break;
-            const int leader = __ffsll((long long)m) - 1;
-            const int r0 = __builtin_amdgcn_readlane(root[k], leader);
-            const unsigned long long same = __ballot(pending && root[k] == r0);
-            if (lane == leader) atomicAdd(lcnt + r0, __popcll(same));
-            if (root[k] == r0) pending = false;
+        // component sizes by horizontal runs: a run (one root) adds its length
+        // once, from its first pixel -- one LDS atomic per run instead of one
+        // per pixel (same-address atomics of a smooth region serialise) or a
+        // ballot loop over the wave's distinct roots (many in a noisy region)
+        const unsigned hm = hrow[ly];
+        const bool start = tx == 0 || !((hm >> (tx - 1)) & 1u);
+        if (root[k] >= 0 && start) {
+            const unsigned rest = ~(hm >> tx);  // bit j: (tx + j) not joined to its right neighbour
+            atomicAdd(lcnt + root[k], __builtin_ctz(rest) + 1);
         }
     }
     __syncthreads();

@@ -18,7 +18,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "mvstereovision3_amd", "csrc")
-DEFAULT = ["mvsv_sgbm.hip", "mvsv_bsgm.hip", "mvsv_bm.hip", "mvsv_post.hip"]
+DEFAULT = ["mvsv_cost.hip", "mvsv_sgbm.hip", "mvsv_bsgm.hip", "mvsv_bm.hip", "mvsv_post.hip"]
 
 
 def demangle(names):
