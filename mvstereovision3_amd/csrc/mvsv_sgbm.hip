@@ -1471,8 +1471,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     using AR = AccRaw<NP, AccT>;
     constexpr int NW = AR::NW;
     // 32 lanes per row: twice the waves, so a shallower prefetch keeps the
-    // kernel at <= 128 VGPRs (4 waves per SIMD)
-    constexpr int PF = LPR == 32 ? MVSV_FINAL32_PF : final16_pf<NP, NACC, AccT, UQ>();
+    // kernel at <= 128 VGPRs (4 waves per SIMD); wide slots (u16 planes of D =
+    // 256, config 5: 12 words per step) take 4 steps -- 8 spilled 14 VGPRs
+    // into scratch (round 6 dispatch census, tests/test_kernel_scratch.py).
+    // The step loop is unrolled by LPR, so PF must divide it.
+    constexpr int kF32Words = (RESF ? 1 : NP) + NACC * AccRaw<NP, AccT>::NW;
+    constexpr int PF = LPR == 32 ? (kF32Words > 10 ? 4 : MVSV_FINAL32_PF) : final16_pf<NP, NACC, AccT, UQ>();
+    static_assert(LPR % PF == 0, "prefetch slots must divide the unrolled step loop");
     constexpr int RPW = 64 / LPR;     // image rows per wave
     constexpr int DR = 2 * NP * LPR;  // disparities of a row (D)
     // S of the current step, one D-vector per row: S[best -+ 1] come back
@@ -2017,6 +2022,16 @@ static int path_schedule(const mvsv_ctx* ctx, const SgbmEff& e, int H, int n)
     if (!ctx->path16 || !(e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256)) return 0;
     const bool dirs_ok = e.P2 <= 15 || ctx->path_sched == 2;  // nibble planes; wider planes when forced
     if (ctx->path_sched == 2) return 2;
+    if (ctx->path_sched == 0 && bsgm_eligible(ctx, e, n, H) && e.SH2 <= 7 && e.SW2 == e.SH2) {
+        // bit-sliced regime (round 6): the side-by-side chains' work grows with
+        // the direction-pixels, the strips' time with the chain length; measured
+        // (8 frames, MI355X r06e): 640x480 5 paths 0.90 side vs 1.11 ms strips,
+        // 8 paths 1.10 vs 1.06; 1280x960 5 paths 3.49 vs 3.07, 8 paths 4.53 vs
+        // 3.20; one 1280x960 frame, 8 paths 0.73 vs 1.03 (round 5)
+        const long long dirpix = (long long)n * e.W1 * H * (e.fullDP ? 8 : 5);
+        if (dirpix <= 12000000LL) return 2;
+        return use_strips(ctx, e, H) ? 1 : 0;
+    }
     if (ctx->path_sched == 0 && dirs_ok) {
         const int wide = e.D > 128 ? 7 : 15;
         const long long blocks = (long long)(e.fullDP ? 2 : 1) * n * ((e.W1 + H - 1 + 4 * wide - 1) / (4 * wide));
@@ -2197,11 +2212,23 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
         // on every SIMD -- launched after the strips on the second stream, the
         // lines fill the strips' step-barrier and hand-off waits (one batch of
         // 8 frames: 4.49 -> 4.37-4.40 ms, MI355X r04d A/B)
+        // Round 6: "small" counts the strip blocks the launch will really have
+        // (launch_tri_lpc picks narrow strips -- 1.7x the blocks -- whenever the
+        // wide ones would not fill the CUs): beside the strips only while those
+        // occupy at most 60 % of the CUs (one 1280x960 frame: 125 narrow D = 256
+        // blocks, 132 narrow D = 128 MODE_HH blocks).  Two config-5 frames (D 256,
+        // 248 narrow blocks) had the lines beside them at 2.68 ms instead of
+        // 0.66 for one frame (r04g c5_frame.jsonl): every CU held a strip.
         int aux_mode = ctx->lines_aux;
         if (aux_mode < 0) {
-            constexpr int wide = tri_wide_waves<NP>();
-            const long long blocks = (long long)npass * n * ((e.W1 + H - 1 + 4 * wide - 1) / (4 * wide));
-            aux_mode = blocks < ctx->cus ? 1 : (RES ? 2 : 0);
+            constexpr int wide = tri_wide_waves<NP>(), narrow = tri_narrow_waves<NP>();
+            auto nblocks = [&](int wv) {
+                return (long long)npass * n * ((e.W1 + H - 1 + 4 * wv - 1) / (4 * wv));
+            };
+            const int wv = ctx->strip_waves == wide || ctx->strip_waves == narrow
+                               ? ctx->strip_waves
+                               : (nblocks(wide) < ctx->cus ? narrow : wide);
+            aux_mode = 5 * nblocks(wv) <= 3 * ctx->cus ? 1 : (RES ? 2 : 0);
         }
         hipStream_t ls = aux_mode ? ctx->aux : s;
         auto lines = [&]() {

@@ -1,4 +1,4 @@
-"""No scratch in the headline pipeline's kernels (CPU test on the built library).
+"""No scratch in the kernels the pipelines dispatch (CPU test on the built library).
 
 Reads the AMDGPU kernel metadata of the gfx950 code objects embedded in
 mvstereovision3_amd/libmvsv.so (.hip_fatbin -> clang offload bundles -> ELF
@@ -8,7 +8,14 @@ sends its spills through scratch, whose evicted lines reach HBM (round 5 found
 the blockSize-13 cost kernel spilling 48 VGPRs: 0.6 GB of extra writes per
 8-frame step; DESIGN.md round-5 summary).  tools/kernel_resources.py lists
 every kernel's registers and scratch from the compiler's remarks.
+
+Round 6: every kernel instance that BASELINE configs 1-5 and the reference's
+call sites (liveDisparity create(0, 64 | 256, 9, 648, 2592), captureDisparity
+create(0, 16, 5, 200, 800)) dispatch at batches of 1, 2 and 8 frames --
+recorded on the GPU by tools/gpu_census.sh into tests/golden/dispatch_census.json
+-- must carry no scratch either.
 """
+import json
 import os
 import re
 import struct
@@ -70,3 +77,28 @@ def test_headline_kernels_have_no_scratch():
         assert any(re.search(p, k) for k in picked), f"no kernel matches {p}"
     bad = {k: v for k, v in picked.items() if v}
     assert not bad, f"headline kernels with scratch: {bad}"
+
+
+CENSUS = os.path.join(ROOT, "tests", "golden", "dispatch_census.json")
+
+
+@pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists(f"{LLVM}/llvm-readelf"),
+                    reason="library not built / no ROCm llvm tools")
+def test_dispatched_kernels_have_no_scratch():
+    ks = kernel_scratch()
+    names = list(ks)
+    dem = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True,
+                         check=True).stdout.splitlines()
+    by_name = dict(zip(dem, names))
+    census = json.load(open(CENSUS))["configs"]
+    assert set(census) >= {"c1", "c2", "c3m0", "c3m1", "c4", "c5", "live64", "capture"}
+    bad, missing = {}, []
+    for cfg, kernels in census.items():
+        for k in kernels:
+            m = by_name.get(k)
+            if m is None:
+                missing.append((cfg, k))
+            elif ks[m]:
+                bad[k] = (cfg, ks[m])
+    assert not missing, f"census kernels not in the library (re-run tools/gpu_census.sh): {missing[:5]}"
+    assert not bad, f"dispatched kernels with scratch: {bad}"
