@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <map>
 #include <sstream>
 #include <string>
@@ -32,6 +33,7 @@ int check_hip(mvsv_ctx* ctx, hipError_t e, const char* what)
 int ensure(mvsv_ctx* ctx, DevBuf& b, size_t bytes, const char* what)
 {
     if (bytes <= b.bytes && b.ptr) return MVSV_OK;
+    ++ctx->alloc_epoch;  // captured graphs hold the old addresses
     if (b.ptr) {
         // the stream may still use the old buffer
         (void)hipStreamSynchronize(ctx->stream);
@@ -222,6 +224,93 @@ int resolve_bm(const mvsv_bm_params* p, int W, int H, BmEff* e, std::string* why
 
 using namespace mvsv;
 
+static void drop_graphs(mvsv_ctx* ctx)
+{
+    for (auto& g : ctx->graph_cache)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    ctx->graph_cache.clear();
+    ctx->graph_seen.clear();
+}
+
+// Replay of repeated small launches as HIP graphs.  `key` holds every argument
+// of the call; the first call with a key runs eagerly, an immediate repeat is
+// captured (on the context's capture stream, so a caller on the legacy null
+// stream is served too) and every later one launches the instantiated graph on
+// the context stream.  Any failure of the capture path turns graphs off for the
+// context and runs the call eagerly.
+constexpr size_t kGraphCache = 4;
+static int graph_run(mvsv_ctx* ctx, const std::vector<unsigned char>& key, const std::function<int()>& body)
+{
+    for (auto& g : ctx->graph_cache) {
+        if (g.key != key) continue;
+        if (g.epoch == ctx->alloc_epoch) {
+            g.used = ++ctx->graph_clock;
+            return check_hip(ctx, hipGraphLaunch(g.exec, ctx->stream), "graph launch");
+        }
+        (void)hipGraphExecDestroy(g.exec);  // its buffers were reallocated
+        g.exec = nullptr;
+        g.key.clear();
+    }
+    if (ctx->graph_seen != key) {
+        ctx->graph_seen = key;
+        return body();
+    }
+    static const bool dbg = std::getenv("MVSV_GRAPH_DEBUG") != nullptr;
+    auto fail = [&]() {
+        const hipError_t le = hipGetLastError();
+        if (dbg) std::fprintf(stderr, "[mvsv graph] capture failed (%s); graphs off for this context\n",
+                              hipGetErrorString(le));
+        ctx->graphs = 0;
+        ctx->graph_seen.clear();
+        return body();
+    };
+    if (!ctx->cap && hipStreamCreateWithFlags(&ctx->cap, hipStreamNonBlocking) != hipSuccess) return fail();
+    const unsigned ep = ctx->alloc_epoch;
+    if (hipStreamBeginCapture(ctx->cap, hipStreamCaptureModeRelaxed) != hipSuccess) return fail();
+    hipStream_t keep = ctx->stream;
+    ctx->stream = ctx->cap;
+    const int rc = body();
+    ctx->stream = keep;
+    hipGraph_t graph = nullptr;
+    const hipError_t ce = hipStreamEndCapture(ctx->cap, &graph);
+    hipGraphExec_t exec = nullptr;
+    const bool ok = rc == MVSV_OK && ce == hipSuccess && graph && ctx->alloc_epoch == ep &&
+                    hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) == hipSuccess;
+    if (graph) (void)hipGraphDestroy(graph);
+    if (!ok) return fail();
+    // keep the kGraphCache most recently used graphs
+    auto slot = ctx->graph_cache.end();
+    for (auto it = ctx->graph_cache.begin(); it != ctx->graph_cache.end(); ++it)
+        if (!it->exec) slot = it;
+    if (slot == ctx->graph_cache.end() && ctx->graph_cache.size() >= kGraphCache) {
+        slot = std::min_element(ctx->graph_cache.begin(), ctx->graph_cache.end(),
+                                [](const mvsv_ctx::GraphEntry& a, const mvsv_ctx::GraphEntry& b) {
+                                    return a.used < b.used;
+                                });
+        (void)hipGraphExecDestroy(slot->exec);
+    }
+    if (slot == ctx->graph_cache.end()) {
+        ctx->graph_cache.emplace_back();
+        slot = ctx->graph_cache.end() - 1;
+    }
+    slot->key = key;
+    slot->exec = exec;
+    slot->epoch = ep;
+    slot->used = ++ctx->graph_clock;
+    ctx->graph_seen.clear();
+    if (dbg)
+        std::fprintf(stderr, "[mvsv graph] captured a %zu-byte key, %zu cached\n", key.size(),
+                     ctx->graph_cache.size());
+    return check_hip(ctx, hipGraphLaunch(exec, ctx->stream), "graph launch");
+}
+
+template <typename T>
+static void key_put(std::vector<unsigned char>& k, const T& v)
+{
+    const unsigned char* p = reinterpret_cast<const unsigned char*>(&v);
+    k.insert(k.end(), p, p + sizeof(T));
+}
+
 extern "C" {
 
 int mvsv_sgbm_validate(const mvsv_sgbm_params* p, int W, int H)
@@ -286,6 +375,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
     if (const char* v = std::getenv("MVSV_STRIP_ORDER")) c->strip_tickets = std::strcmp(v, "blockidx") != 0;
     if (const char* v = std::getenv("MVSV_LINES_AUX")) c->lines_aux = std::max(-1, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("MVSV_BITSLICE")) c->bitslice = std::atoi(v) != 0;
+    if (const char* v = std::getenv("MVSV_GRAPHS")) c->graphs = std::atoi(v) != 0;
     if (const char* v = std::getenv("MVSV_BS_SERIAL")) c->bs_serial = std::atoi(v) != 0;
     if (const char* v = std::getenv("MVSV_COST_XCD")) c->cost_xcd = std::atoi(v) != 0;
     if (const char* v = std::getenv("MVSV_BS_FUSE")) c->bs_fuse = std::atoi(v) != 0;
@@ -299,7 +389,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
 
 static void free_buf(DevBuf& b)
 {
-    if (b.ptr) (void)hipFree(b.ptr);
+    if (b.ptr) (void)hipFree(b.ptr);  // (the caller bumps alloc_epoch)
     b.ptr = nullptr;
     b.bytes = 0;
 }
@@ -307,6 +397,7 @@ static void free_buf(DevBuf& b)
 int mvsv_trim(mvsv_ctx* ctx)
 {
     if (!ctx) return MVSV_E_INVALID_ARG;
+    ++ctx->alloc_epoch;
     DeviceGuard dev_guard(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     DevBuf* all[] = {&ctx->pre, &ctx->cost, &ctx->cres, &ctx->agg, &ctx->raw, &ctx->uf_parent, &ctx->uf_size, &ctx->uf_lroot, &ctx->uf_list,
@@ -372,7 +463,9 @@ int mvsv_profile_read(mvsv_ctx* ctx, double* ms, int* launches, int n)
 void mvsv_destroy(mvsv_ctx* ctx)
 {
     if (!ctx) return;
+    drop_graphs(ctx);
     mvsv_trim(ctx);
+    if (ctx->cap) (void)hipStreamDestroy(ctx->cap);
     mvsv_profile_reset(ctx);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
@@ -512,7 +605,28 @@ int mvsv_sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t l
     // maps are INVALID; say so before anything else runs on this context
     if ((rc = check_report(ctx))) return rc;
     DeviceGuard dev_guard(ctx->device);
-    return mark_last_use(ctx, sgbm_device(ctx, n, L, ls, lfs, R, rs, rfs, W, H, e, out, os, ofs));
+    auto body = [&]() { return sgbm_device(ctx, n, L, ls, lfs, R, rs, rfs, W, H, e, out, os, ofs); };
+    // small launches (one camera frame): one graph launch instead of ~8 kernel
+    // launches (config 3, one 640x480 frame: ~5 us of launch gap per kernel)
+    if (ctx->graphs && !ctx->prof && sgbm_graphable(ctx, e, n, H)) {
+        std::vector<unsigned char> key;
+        key_put(key, 'S');
+        key_put(key, n);
+        key_put(key, L);
+        key_put(key, ls);
+        key_put(key, lfs);
+        key_put(key, R);
+        key_put(key, rs);
+        key_put(key, rfs);
+        key_put(key, W);
+        key_put(key, H);
+        key_put(key, e);
+        key_put(key, out);
+        key_put(key, os);
+        key_put(key, ofs);
+        return mark_last_use(ctx, graph_run(ctx, key, body));
+    }
+    return mark_last_use(ctx, body());
 }
 
 int mvsv_bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs,
@@ -528,7 +642,28 @@ int mvsv_bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs
     int rc = resolve_bm(p, W, H, &e, &why);
     if (rc) return set_error(ctx, rc, why);
     DeviceGuard dev_guard(ctx->device);
-    return mark_last_use(ctx, bm_device(ctx, n, L, ls, lfs, R, rs, rfs, W, H, e, out, os, ofs));
+    auto body = [&]() { return bm_device(ctx, n, L, ls, lfs, R, rs, rfs, W, H, e, out, os, ofs); };
+    // StereoBM launches carry no per-launch state: repeats replay as a graph
+    // (config 2, one 640x480 frame: 0.045 ms per call, ~6 kernel launches)
+    if (ctx->graphs && !ctx->prof) {
+        std::vector<unsigned char> key;
+        key_put(key, 'B');
+        key_put(key, n);
+        key_put(key, L);
+        key_put(key, ls);
+        key_put(key, lfs);
+        key_put(key, R);
+        key_put(key, rs);
+        key_put(key, rfs);
+        key_put(key, W);
+        key_put(key, H);
+        key_put(key, e);
+        key_put(key, out);
+        key_put(key, os);
+        key_put(key, ofs);
+        return mark_last_use(ctx, graph_run(ctx, key, body));
+    }
+    return mark_last_use(ctx, body());
 }
 
 int mvsv_mean_disparity_grid_device(mvsv_ctx* ctx, int n, const int16_t* dmap, size_t st,

@@ -133,6 +133,25 @@ struct mvsv_ctx {
     int bm2 = 1;     // StereoBM: disparities-on-lanes match kernel where blockSize <= 21, D <= 128
     int bm_ty = 0;   // its tile height (0 = chosen per launch); MVSV_BM_TY for A/B runs
     int cus = 256;   // compute units of the device (launch-shape choices)
+    // HIP graphs (round 6): a small SGBM launch (no strip chain, whose launches
+    // carry per-launch epochs) repeated with the same arguments is captured once
+    // on the capture stream and then replayed as one graph launch; every cached
+    // buffer (re)allocation or free bumps alloc_epoch and retires the graphs
+    // measured slower than eager launches on ROCm 7.2 / MI355X (config 3 one
+    // frame 0.259 vs 0.250 ms, config 2 0.041 vs 0.033 ms; profiles/r06/graphs),
+    // so opt-in: MVSV_GRAPHS=1
+    int graphs = 0;
+    unsigned alloc_epoch = 0;
+    struct GraphEntry {
+        std::vector<unsigned char> key;
+        hipGraphExec_t exec = nullptr;
+        unsigned epoch = 0;
+        unsigned long long used = 0;
+    };
+    std::vector<GraphEntry> graph_cache;
+    std::vector<unsigned char> graph_seen;  // arguments of the last eager launch
+    unsigned long long graph_clock = 0;
+    hipStream_t cap = nullptr;  // capture stream
     // BM
     mvsv::DevBuf bm_lf, bm_rf, bm_cost, bm_sad;
     // host-pointer staging
@@ -188,6 +207,9 @@ struct StageTimer {
 int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, const uint8_t* R,
                 size_t rs, size_t rfs, int W, int H, const SgbmEff& e, int16_t* out, size_t os,
                 size_t ofs);
+// the launch runs no strip chain (path schedule 2): its kernels and arguments are
+// the same on every call with the same arguments, so it may be replayed as a graph
+bool sgbm_graphable(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H);
 int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, const uint8_t* R,
               size_t rs, size_t rfs, int W, int H, const BmEff& e, int16_t* out, size_t os,
               size_t ofs);

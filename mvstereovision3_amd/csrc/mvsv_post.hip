@@ -141,6 +141,19 @@ __device__ __forceinline__ int lfind(int* par, int i)
     return i;
 }
 
+// the root without path compression: the lanes of a wave mostly walk the same
+// chains, and the compressing atomicMin of lfind serialised them on one LDS
+// address (0.51 of the kernel's LDS cycles were bank conflicts, round 5)
+__device__ __forceinline__ int lroot_ro(const int* par, int i)
+{
+    int p = lds_load(par + i);
+    for (;;) {
+        const int q = lds_load(par + p);
+        if (q == p) return p;
+        p = q;
+    }
+}
+
 __device__ void lunite(int* par, int a, int b)
 {
     for (;;) {
@@ -225,7 +238,7 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(int16_t* __restrict_
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int ly = ty + 8 * k, li = ly * kSpTile + tx;
-        root[k] = lval[li] != kInvalid ? lfind(lpar, li) : -1;
+        root[k] = lval[li] != kInvalid ? lroot_ro(lpar, li) : -1;
         // component sizes by horizontal runs: a run (one root) adds its length
         // once, from its first pixel -- one LDS atomic per run instead of one
         // per pixel (same-address atomics of a smooth region serialise) or a
@@ -237,12 +250,21 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(int16_t* __restrict_
             atomicAdd(lcnt + root[k], __builtin_ctz(rest) + 1);
         }
     }
+    __shared__ unsigned s_roots, s_base;
+    if (threadIdx.x == 0) s_roots = 0u;
     __syncthreads();
     const size_t npix = (size_t)W * H;
     int* par = parent + f * npix;
     int* tl = tilew + f * npix;
     int* sz = size + f * npix;
     uint16_t* lr = lroot + f * npix;
+    // the tile's components go to the compact root list (list[0] = count) with
+    // ONE global atomic per block: every block appending per wave and row group
+    // put 16 same-address L2 atomics per tile on list[0], serialised across the
+    // whole launch (9 600 tiles per 8-frame step)
+    unsigned long long rm[4];
+    unsigned roff[4];
+    int rgi[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int ly = ty + 8 * k, li = ly * kSpTile + tx;
@@ -257,17 +279,25 @@ __global__ __launch_bounds__(256) void speckle_local_kernel(int16_t* __restrict_
             tl[gi] = c;
             sz[gi] = 0;
         }
-        // wave-aggregated append to the compact root list (list[0] = count)
-        const unsigned long long m = __ballot(isroot);
-        if (m) {
-            const int leader = __ffsll((long long)m) - 1;
-            unsigned base = 0;
-            if (lane == leader) base = atomicAdd(list, (unsigned)__popcll(m));
-            base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
-            if (isroot)
-                list[1 + base + (unsigned)__popcll(m & ((1ull << lane) - 1ull))] = (unsigned)(f * npix + gi);
+        rgi[k] = isroot ? gi : -1;
+        rm[k] = __ballot(isroot);
+        roff[k] = 0;
+        if (rm[k]) {
+            const int leader = __ffsll((long long)rm[k]) - 1;
+            unsigned o = 0;
+            if (lane == leader) o = atomicAdd(&s_roots, (unsigned)__popcll(rm[k]));  // LDS
+            roff[k] = (unsigned)__builtin_amdgcn_readlane((int)o, leader);
         }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_roots ? atomicAdd(list, s_roots) : 0u;
+    __syncthreads();
+    const unsigned base = s_base;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (rgi[k] >= 0)
+            list[1 + base + roff[k] + (unsigned)__popcll(rm[k] & ((1ull << lane) - 1ull))] =
+                (unsigned)(f * npix + rgi[k]);
 }
 
 // Union-find over tile components (the global parent words of tile roots).

@@ -2418,6 +2418,11 @@ int launch_paths_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
 
 }  // namespace
 
+bool sgbm_graphable(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H)
+{
+    return e.minX1 < e.maxX1 && e.D <= 512 && path_schedule(ctx, e, H, n) == 2;
+}
+
 int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, const uint8_t* R,
                 size_t rs, size_t rfs, int W, int H, const SgbmEff& e, int16_t* out, size_t os,
                 size_t ofs)
