@@ -119,7 +119,7 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True, res=False, bits=False):
+def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True, res=False, bits=False, side=False):
     """Implementation HBM bytes of one step per stage ("Kernels").
 
     acc = bytes per (pixel, disparity) of a path-delta accumulator plane (0.5 for
@@ -134,14 +134,28 @@ def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True, res=False, bits=F
     cost kernel writes C (read back only at best -+ 1) and the 4-bit C' planes,
     the strip passes read C' and write a 4-bit plane each, the L->R lines read
     C' and write a 3-bit plane, the R->L lines fused with the WTA read C', the
-    three planes and the gathered costs.
+    three planes and the gathered costs.  bits + side = the bit-sliced
+    small-launch form: every direction on its own chains writing a grouped 3-bit
+    delta plane (48 B per padded pixel), the WTA reading C' and all of them.
+    (Which form runs is what the library reports, mvsv_sgbm_plan.)
     """
     cells = W1 * H * D
     px = W * H
     npass = 2 if ndir == 8 else 1
     cin = 0.5 if res else 2
+    if bits and side:
+        W1q = (W1 + 3) // 4 * 4
+        dirs_b = F * ndir * (W1q * H * 64 + W1q * H * 48)  # each chain reads C', writes its plane
+        return {
+            "prefilter": F * (2 * px + 2 * 8 * px),
+            "cost_volume": F * (2 * 8 * px + 2.5 * cells + 2 * W1 * H),
+            "path_aggregation": dirs_b,
+            "final_wta_lr": F * (W1q * H * (64 + ndir * 48) + W1 * H * (2 + 8) + 6 * px),
+            "post_filters": F * 4 * px,
+        }.get(stage, 0)
     if bits:
-        strip_b = F * cells * 2 * (0.5 + 0.5)
+        npb = 2 if ndir == 8 else 1  # strip passes (MODE_SGBM: down only)
+        strip_b = F * cells * npb * (0.5 + 0.5)
         lines_b = F * cells * (0.5 + 0.375)  # L->R only: R->L runs with the WTA
         return {
             "prefilter": F * (2 * px + 2 * 8 * px),
@@ -152,7 +166,7 @@ def stage_bytes(stage, F, W, H, W1, D, ndir, acc, strips=True, res=False, bits=F
             # R->L + WTA: C', two strip planes, the L->R plane, a 4-byte record
             # per pixel written and read back; the finish: minimum, gathered
             # costs, raw map and right-view keys per pixel
-            "final_wta_lr": F * (cells * (0.5 + 2 * 0.5 + 0.375) + W1 * H * (8 + 2 + 8) + 6 * px),
+            "final_wta_lr": F * (cells * (0.5 + npb * 0.5 + 0.375) + W1 * H * (8 + 2 + 8) + 6 * px),
             "post_filters": F * 4 * px,
         }.get(stage, 0)
     if strips:
@@ -474,17 +488,13 @@ def main(argv=None):
     # bytes per (pixel, disparity) of an accumulator plane: 4-bit planes on the
     # strip schedule when 3 * P2 <= 15 (sgbm.yml: P2 = 5), else u8 / u16
     acc = 0.5 if (D in (32, 64, 128, 256) and 3 * P2 <= 15) else (1 if ndir * P2 <= 255 else 2)
-    # the cost residual plane (mvsv.h MVSV_OPT_COST_RESIDUAL): no-wrap bound,
-    # 3 * P2 <= 15, D <= 128 -- sgbm.yml
-    bs = params["block_size"] if params["block_size"] > 0 else 5
-    ftzero = max(params["pre_filter_cap"], 15) | 1
-    residual = (os.environ.get("MVSV_COST_RESIDUAL", "1") != "0" and D in (32, 64, 128) and 3 * P2 <= 15
-                and 2 * P2 + bs * bs * (2 * ftzero + 63) <= 32767)
-    # the bit-sliced MODE_HH pipeline (MVSV_OPT_BITSLICE; frame batches on the
-    # strip schedule): sgbm.yml's P1 2 / P2 5, D 128, uniquenessRatio 0
-    uq = params["uniqueness_ratio"]
-    bitslice = (os.environ.get("MVSV_BITSLICE", "1") != "0" and ndir == 8 and D == 128 and P1 == 2 and P2 == 5
-                and uq == 0 and 2 * P2 + bs * bs * (2 * ftzero + 63) <= 32767 and F >= 2)
+    # the pipeline the library will run for this launch, as it reports it
+    # (mvsv_sgbm_plan): bit-sliced (MODE_HH or MODE_SGBM, sgbm.yml's regime),
+    # side by side or strips, the nibble residual plane of the packed passes
+    plan = _lib.sgbm_plan(_lib.context(dev.index or 0), F, W, H, m._params)
+    bitslice = bool(plan & _lib.PLAN_BITSLICE)
+    side = bool(plan & _lib.PLAN_SIDE)
+    residual = bool(plan & _lib.PLAN_RESIDUAL)
 
     from mvstereovision3_amd.batch import FrameBatch, InflightBatches, frame_seeds
     host = [mvsv.synth_pair(sd, W, H, minD, D) for sd in frame_seeds(rank, world, F, SEED0)]
@@ -579,7 +589,8 @@ def main(argv=None):
         comp = 4 * W * H * (1 + D)
         alg_bytes_per_launch = comp * F / launches
         achieved = alg_bytes_per_launch / avg_launch_s / 1e9
-        impl_bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir, acc, strips, residual, bitslice) / launches
+        impl_bytes_per_launch = stage_bytes(dom, F, W, H, W1, D, ndir, acc, strips, residual, bitslice,
+                                            side) / launches
         workload = f"sgbm_{W}x{H}_d{D}_{ndir}path_batch{F}"
         sha = kernel_source_sha()
         pmc, traffic_note = _summary(PMC_FILE, workload, sha, "PMC")

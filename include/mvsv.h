@@ -235,6 +235,18 @@ MVSV_API int mvsv_bm_device(mvsv_ctx* ctx, int n, const uint8_t* left, size_t le
 MVSV_API size_t mvsv_sgbm_workspace_bytes(int n, int width, int height,
                                           const mvsv_sgbm_params* p);
 
+/* The pipeline this context would run for an SGBM call of this shape and these
+   parameters (no reference counterpart: introspection for byte models and
+   tests), as MVSV_PLAN_* bits in *plan. */
+enum {
+    MVSV_PLAN_BITSLICE = 1,  /* bit-sliced path aggregation (MODE_HH or MODE_SGBM, sgbm.yml regime) */
+    MVSV_PLAN_SIDE = 2,      /* every direction on its own chains (small launches) */
+    MVSV_PLAN_STRIPS = 4,    /* sheared strips + row directions (frame batches) */
+    MVSV_PLAN_RESIDUAL = 8   /* packed passes read the nibble cost residual plane */
+};
+MVSV_API int mvsv_sgbm_plan(mvsv_ctx* ctx, int n, int width, int height, const mvsv_sgbm_params* p,
+                            int* plan);
+
 /* MeanDisparityDetection post-pass on device: 9x9 tile means of an int16 map
  * (tile = (W/9)x(H/9), remainder ignored; mean over values > 1 with integer
  * division, 0 for an empty tile).  means: 81 floats per frame (device ptr). */

@@ -124,6 +124,7 @@ def _declare(lib, strict=True):
         "mvsv_sgbm_device": ([P, I, P, Z, Z, P, Z, Z, I, I, P, P, Z, Z], I),
         "mvsv_bm_device": ([P, I, P, Z, Z, P, Z, Z, I, I, P, P, Z, Z], I),
         "mvsv_sgbm_workspace_bytes": ([I, I, I, P], Z),
+        "mvsv_sgbm_plan": ([P, I, I, I, P, P], I),
         "mvsv_mean_disparity_grid_device": ([P, I, P, Z, Z, I, I, P], I),
         "mvsv_load_sgbm_yaml": ([ctypes.c_char_p, P, P], I),
         "mvsv_load_bm_yaml": ([ctypes.c_char_p, P], I),
@@ -285,3 +286,14 @@ def profile_read(ctx: Context) -> dict:
     n = (ctypes.c_int * NUM_STAGES)()
     check(lib().mvsv_profile_read(ctx.handle, ms, n, NUM_STAGES), ctx.handle)
     return {lib().mvsv_profile_stage_name(i).decode(): (ms[i], n[i]) for i in range(NUM_STAGES)}
+
+
+PLAN_BITSLICE, PLAN_SIDE, PLAN_STRIPS, PLAN_RESIDUAL = 1, 2, 4, 8
+
+
+def sgbm_plan(ctx, n, width, height, params) -> int:
+    """MVSV_PLAN_* bits of the pipeline ``ctx`` runs for an SGBM call of this
+    shape (mvsv_sgbm_plan): bit-sliced, side by side / strips, residual plane."""
+    out = ctypes.c_int(0)
+    check(lib().mvsv_sgbm_plan(ctx.handle, n, width, height, ctypes.byref(params), ctypes.byref(out)), ctx.handle)
+    return out.value

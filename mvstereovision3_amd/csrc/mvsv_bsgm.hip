@@ -1156,10 +1156,18 @@ static int launch_bs_strips(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const
     const dim3 grid(nstrips * npass * n);
     const bool tickets = ctx->strip_tickets != 0;
     // MVSV_BS_STATS: per-strip spans and hand-off spin time on stderr
+    // (diagnostics only: the buffer is cleared on the context stream, and any
+    // failure turns the statistics off instead of touching a null buffer)
     unsigned long long* stats = nullptr;
     if (std::getenv("MVSV_BS_STATS")) {
-        (void)hipMalloc(&stats, (size_t)grid.x * 64);
-        (void)hipMemset(stats, 0, (size_t)grid.x * 64);
+        if (hipMalloc(&stats, (size_t)grid.x * 64) != hipSuccess) {
+            (void)hipGetLastError();
+            stats = nullptr;
+        } else if (hipMemsetAsync(stats, 0, (size_t)grid.x * 64, ctx->stream) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(stats);
+            stats = nullptr;
+        }
     }
     // one strip block per CU: dynamic LDS past half the CU's 160 KiB (a second
     // strip block on the same CU makes that CU's strips, and every strip left of
@@ -1181,10 +1189,14 @@ static int launch_bs_strips(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const
     rc = check_hip(ctx, hipGetLastError(), "bit-sliced strip kernel");
     if (rc == MVSV_OK && tickets) ctx->tri_tickets += grid.x;
     if (stats) {
-        (void)hipStreamSynchronize(ctx->stream);
         std::vector<unsigned long long> hv((size_t)grid.x * 8);
-        (void)hipMemcpy(hv.data(), stats, hv.size() * 8, hipMemcpyDeviceToHost);
+        const bool ok = hipStreamSynchronize(ctx->stream) == hipSuccess &&
+                        hipMemcpy(hv.data(), stats, hv.size() * 8, hipMemcpyDeviceToHost) == hipSuccess;
         (void)hipFree(stats);
+        if (!ok) {
+            (void)hipGetLastError();
+            return rc;
+        }
         unsigned long long t0 = ~0ull, t1 = 0, spin = 0, busy = 0, steps = 0;
         for (size_t b = 0; b < grid.x; b++) {
             const unsigned long long* q = &hv[b * 8];

@@ -887,6 +887,16 @@ int launch_cost(mvsv_ctx* ctx, int n, int W, int H, const SgbmEff& e, int TY,
     return check_hip(ctx, hipGetLastError(), "sgbm cost kernel");
 }
 
+bool cost2_runs(const mvsv_ctx* ctx, const SgbmEff& e)
+{
+    if (!ctx->cost2 || e.SH2 > 7 || e.SW2 != e.SH2) return false;
+    const Cost2Layout l2 = cost2_layout(e.D, e.SW2, 120);  // (the layout does not depend on the tile height)
+    const int items = 2 * l2.NX + e.D - 1;
+    const int ppc = !ctx->cost_fixed_pp ? 0 : l2.PP == 64 ? 64 : (l2.PP == 128 ? 128 : 0);
+    const size_t lbytes = cost2_total_bytes(l2, 2 * e.SH2 + 1, items > kCost2Threads ? 2 : 1, ppc);
+    return l2.CL >= 1 && items <= kCost2Threads * 2 && lbytes <= 160 * 1024;
+}
+
 int launch_prefilter(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, const uint8_t* R, size_t rs,
                      size_t rfs, int W, int H, int ftzero, uint64_t* pre)
 {

@@ -589,6 +589,17 @@ size_t mvsv_sgbm_workspace_bytes(int n, int W, int H, const mvsv_sgbm_params* p)
     return b;
 }
 
+int mvsv_sgbm_plan(mvsv_ctx* ctx, int n, int W, int H, const mvsv_sgbm_params* p, int* plan)
+{
+    if (!ctx || !plan || n <= 0) return MVSV_E_INVALID_ARG;
+    SgbmEff e;
+    std::string why;
+    const int rc = resolve_sgbm(p, W, H, &e, &why);
+    if (rc) return set_error(ctx, rc, why);
+    *plan = sgbm_plan(ctx, e, n, H);
+    return MVSV_OK;
+}
+
 int mvsv_sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs,
                      const uint8_t* R, size_t rs, size_t rfs, int W, int H,
                      const mvsv_sgbm_params* p, int16_t* out, size_t os, size_t ofs)

@@ -210,6 +210,10 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
 // the launch runs no strip chain (path schedule 2): its kernels and arguments are
 // the same on every call with the same arguments, so it may be replayed as a graph
 bool sgbm_graphable(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H);
+// MVSV_PLAN_* bits of the pipeline sgbm_device runs for these arguments
+int sgbm_plan(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H);
+// the register-ring cost kernel runs (and can write the bit-sliced planes)
+bool cost2_runs(const mvsv_ctx* ctx, const SgbmEff& e);
 int bm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, const uint8_t* R,
               size_t rs, size_t rfs, int W, int H, const BmEff& e, int16_t* out, size_t os,
               size_t ofs);

@@ -2418,6 +2418,17 @@ int launch_paths_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
 
 }  // namespace
 
+int sgbm_plan(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H)
+{
+    if (e.minX1 >= e.maxX1) return 0;
+    const int sched = path_schedule(ctx, e, H, n);
+    const bool bs = bsgm_eligible(ctx, e, n, H) && (sched == 1 || sched == 2) && ctx->path16 && ctx->tri &&
+                    ctx->cost_fixed_pp && e.SH2 <= 7 && e.SW2 == e.SH2 && cost2_runs(ctx, e);
+    int plan = (bs ? MVSV_PLAN_BITSLICE : 0) | (sched == 2 ? MVSV_PLAN_SIDE : 0) | (sched == 1 ? MVSV_PLAN_STRIPS : 0);
+    if (!bs && use_residual(ctx, e, sched) && cost2_runs(ctx, e)) plan |= MVSV_PLAN_RESIDUAL;
+    return plan;
+}
+
 bool sgbm_graphable(const mvsv_ctx* ctx, const SgbmEff& e, int n, int H)
 {
     return e.minX1 < e.maxX1 && e.D <= 512 && path_schedule(ctx, e, H, n) == 2;

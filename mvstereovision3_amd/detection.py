@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 import weakref
 
 import numpy as np
@@ -228,6 +229,9 @@ class DisparityStream:
         # the last view is gone (use-after-free otherwise)
         self._live_views = 0
         self._close_pending = False
+        # pop views are released by weakref finalizers, which may run from GC on
+        # any thread: the view count, the pending close and the destroy share a lock
+        self._views_lock = threading.RLock()
         if batch != 1:
             self.set_batch(batch)
         if inflight != 1:
@@ -280,8 +284,10 @@ class DisparityStream:
                   self._ctx.handle)
             buf = (ctypes.c_int16 * (self.width * self.height)).from_address(ptr.value)
             buf._owner = self  # numpy's base chain keeps the stream (and its slots) alive
-            self._live_views += 1
-            weakref.finalize(buf, DisparityStream._view_released, self)
+            with self._views_lock:
+                self._live_views += 1
+            fin = weakref.finalize(buf, DisparityStream._view_released, self)
+            fin.atexit = False  # no library calls during interpreter shutdown
             view = np.ctypeslib.as_array(buf).reshape(self.height, self.width)
             view.flags.writeable = False
             return view, means
@@ -294,22 +300,25 @@ class DisparityStream:
 
     @staticmethod
     def _view_released(stream):
-        stream._live_views -= 1
-        if stream._close_pending and stream._live_views == 0:
-            stream._destroy()
+        with stream._views_lock:
+            stream._live_views -= 1
+            if stream._close_pending and stream._live_views == 0:
+                stream._destroy()
 
     def _destroy(self):
-        if self._h:
-            lib().mvsv_stream_destroy(self._h)
-            self._h = None
-        self._close_pending = False
+        with self._views_lock:
+            if self._h:
+                lib().mvsv_stream_destroy(self._h)
+                self._h = None
+            self._close_pending = False
 
     def close(self):
         """Destroys the stream; with pop views still alive, when the last one goes."""
-        if self._live_views > 0:
-            self._close_pending = True
-            return
-        self._destroy()
+        with self._views_lock:
+            if self._live_views > 0:
+                self._close_pending = True
+                return
+            self._destroy()
 
     @property
     def closed(self):

@@ -162,6 +162,24 @@ int main()
                             shapes++;
                         }
             }
+    // the register-ring kernel (and with it the bit-sliced planes and the
+    // residual plane) must launch for every window of D = 128 / 256 at every
+    // tile height: its LDS -- layout + the LDS ring slots -- fits a CU (a
+    // shape that did not would fall back to the LDS-ring kernel silently;
+    // ADVICE r05).  Mirrors launch_cost / cost2_runs in mvsv_cost.hip.
+    for (int D : {128, 256})
+        for (int SW2 = 0; SW2 <= 7; SW2++)
+            for (int TY : tys) {
+                const Cost2Layout l2 = cost2_layout(D, SW2, TY);
+                const int items = 2 * l2.NX + D - 1;
+                const int ppc = l2.PP == 64 ? 64 : (l2.PP == 128 ? 128 : 0);
+                const size_t lbytes = cost2_total_bytes(l2, 2 * SW2 + 1, items > kCost2Threads ? 2 : 1, ppc);
+                if (!(l2.CL >= 1 && items <= 2 * kCost2Threads && lbytes <= 160 * 1024)) {
+                    std::printf("register-ring cost kernel does not fit: D %d blockSize %d TY %d (%zu B)\n", D,
+                                2 * SW2 + 1, TY, lbytes);
+                    violations++;
+                }
+            }
     std::printf("cost_layout_check: %lld shapes, %lld violations\n", shapes, violations);
     return violations ? 1 : 0;
 }

@@ -187,3 +187,26 @@ def test_bitslice_workspace_bound(gpu, mvsv, shape):
         ctx.close()
     # allocation granularity / runtime slack: 64 MB
     assert used <= est + (64 << 20), f"context used {used} B, workspace estimate {est} B"
+
+
+def test_sgbm_plan_reports_the_pipeline(gpu, mvsv):
+    """mvsv_sgbm_plan (what bench.py's byte model reads): the bit-sliced strips
+    for the headline batch, the bit-sliced side-by-side chains for one camera
+    frame and for the 5-path 640x480 batch, the packed strips with the residual
+    plane when bit-slicing is off, and no bit-slicing for config 5."""
+    from mvstereovision3_amd import _lib
+    ctx = _lib.context(0)
+    hh = mvsv.StereoSGBM.create(1, 128, 13, 0, 0, 0, 0, 0, 150, 2, 1)
+    sg = mvsv.StereoSGBM.create(1, 128, 13, 0, 0, 0, 0, 0, 150, 2, 0)
+    c5 = mvsv.StereoSGBM.create(0, 256, 9, 648, 2592)
+    B, SIDE, STRIPS, RES = _lib.PLAN_BITSLICE, _lib.PLAN_SIDE, _lib.PLAN_STRIPS, _lib.PLAN_RESIDUAL
+    assert _lib.sgbm_plan(ctx, 8, 1280, 960, hh._params) == B | STRIPS
+    assert _lib.sgbm_plan(ctx, 8, 1280, 960, sg._params) == B | STRIPS
+    assert _lib.sgbm_plan(ctx, 1, 640, 480, hh._params) == B | SIDE
+    assert _lib.sgbm_plan(ctx, 8, 640, 480, sg._params) == B | SIDE
+    assert _lib.sgbm_plan(ctx, 8, 1280, 960, c5._params) & B == 0
+    try:
+        _lib.set_option(_lib.OPT_BITSLICE, 0)
+        assert _lib.sgbm_plan(ctx, 8, 1280, 960, hh._params) == STRIPS | RES
+    finally:
+        _lib.set_option(_lib.OPT_BITSLICE, 1)

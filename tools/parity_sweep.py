@@ -135,8 +135,9 @@ def main():
     _lib.set_option(_lib.OPT_STRIP_TICKETS, 1)
     _lib.set_option(_lib.OPT_COST_RESIDUAL, 1)
 
-    # the bit-sliced MODE_HH pipeline (round 5): strips + fused R->L / WTA for
-    # batches, the side-by-side chains for small launches, forced off
+    # the bit-sliced pipeline (round 5 MODE_HH, round 6 MODE_SGBM): strips +
+    # fused R->L / WTA for batches, the side-by-side chains for small launches,
+    # forced off
     for i in range(a.bits + a.bits_large):
         large = i >= a.bits
         if large:
@@ -151,7 +152,8 @@ def main():
         kw = dict(minDisparity=minD, numDisparities=128, blockSize=int(rng.choice([0, 1, 3, 5, 9, 13, 15])),
                   P1=int(rng.choice([0, 2])), P2=int(rng.choice([0, 5])), disp12MaxDiff=int(rng.integers(-1, 4)),
                   preFilterCap=int(rng.choice([0, 15, 31, 63])), uniquenessRatio=0,
-                  speckleWindowSize=int(rng.choice([0, 0, 20, 150])), speckleRange=int(rng.choice([1, 2, 4])), mode=1)
+                  speckleWindowSize=int(rng.choice([0, 0, 20, 150])), speckleRange=int(rng.choice([1, 2, 4])),
+                  mode=int(rng.integers(0, 2)))  # round 6: MODE_SGBM is bit-sliced too
         variant = int(rng.integers(0, 4))
         sched = int(rng.choice([0, 0, 1, 2]))
         bits = int(rng.choice([1, 1, 1, 0]))
