@@ -321,6 +321,22 @@ def config_table(mvsv, _lib, dev, steps=10, warmup=3):
         add(f"config5_sgbm_1280x960_d256_batch{n}", 1280, 960, 256, n, ms,
             ("sgbm5", OPS_PER_PXD["sgbm5"] * 1280 * 960 * 256 * n), pairs[0], out[0].cpu().numpy(),
             (lambda L0, R0, p=p256: pyoracle.sgbm(L0, R0, p)) if n == 1 else None, {"mode": "MODE_SGBM"})
+    # the reference's other call sites: liveDisparity's
+    # default create(0, 64, 9, 648, 2592) (trgt/liveDisparity.cpp:19-20,61) at
+    # 1280x960 and captureDisparity's create(0, 16, 5, 200, 800)
+    # (trgt/captureDisparity.cpp:24-25,196) at 640x480, one frame and a batch of 8
+    for name, (mn, nd, bsz, p1, p2), (W, H) in (
+            ("live_default_sgbm_d64_bs9", (0, 64, 9, 648, 2592), (1280, 960)),
+            ("capture_sgbm_d16_bs5", (0, 16, 5, 200, 800), (640, 480))):
+        mc = mvsv.StereoSGBM.create(mn, nd, bsz, p1, p2)
+        pc = {k: v for k, v in mc.params().items() if k != "variant"}
+        for n in (1, 8):
+            pairs, L, R = frames(n, W, H, mn, nd)
+            out = torch.empty((n, H, W), dtype=torch.int16, device=dev)
+            ms = timed(lambda: mc.compute(L, R, out))
+            add(f"{name}_{W}x{H}_batch{n}", W, H, nd, n, ms, ("sgbm5", OPS_PER_PXD["sgbm5"] * W * H * nd * n),
+                pairs[0], out[0].cpu().numpy(),
+                (lambda L0, R0, p=pc: pyoracle.sgbm(L0, R0, p)) if n == 1 else None, {"mode": "MODE_SGBM"})
     # config 5 as BASELINE states it: the sustained stream (host frames in, maps and
     # the 81 MeanDisparityDetection means out, the detection post-pass on every
     # frame; trgt/liveDisparity.cpp:61,82-101, src/MeanDisparityDetection.cpp:159-266)
