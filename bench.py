@@ -54,7 +54,7 @@ if ROOT not in sys.path:
 SEED0 = 0x5EED0000
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SGBM_YML = os.path.join(ROOT, "tests", "golden", "configs", "sgbm.yml")
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r06")
 PMC_FILE = os.path.join(PROFILE_DIR, "pmc_traffic.json")  # tools/pmc_traffic.py
 SQ_FILE = os.path.join(PROFILE_DIR, "sq_summary.json")    # tools/sq_summary.py
 KERNEL_SOURCES = os.path.join(ROOT, "mvstereovision3_amd", "csrc")

@@ -1304,9 +1304,15 @@ int bsgm_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16
         if (side && (rc = lines())) return rc;
         {
             StageTimer ts(ctx, kStageStrips);
-            const int ng = ctx->bs_groups;
+            // 3 column groups (96 U-columns, 10 waves) for MODE_HH batches: 352
+            // strip blocks per 8-frame batch instead of 528 overlap better with
+            // the other batch in flight (bench 3114-3120 -> 3164-3169 Mpix/s,
+            // same box, r06n; one batch alone: strips 1.14 -> 1.15 ms); 4 groups
+            // leave no room for the line waves beside them (lines 0.55 -> 2.0 ms)
+            const int ng = ctx->bs_groups ? ctx->bs_groups : (e.fullDP ? 3 : 2);
             uint32_t* dummy = Dv + 2 * dplane;
             rc = ng == 1   ? launch_bs_strips<1>(ctx, n, H, e, Bv, Av, aplane, dummy)
+                 : ng == 3 ? launch_bs_strips<3>(ctx, n, H, e, Bv, Av, aplane, dummy)
                  : ng == 4 ? launch_bs_strips<4>(ctx, n, H, e, Bv, Av, aplane, dummy)
                  : ng == 5 ? launch_bs_strips<5>(ctx, n, H, e, Bv, Av, aplane, dummy)
                            : launch_bs_strips<2>(ctx, n, H, e, Bv, Av, aplane, dummy);

@@ -381,7 +381,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
     if (const char* v = std::getenv("MVSV_BS_FUSE")) c->bs_fuse = std::atoi(v) != 0;
     if (const char* v = std::getenv("MVSV_BS_GROUPS")) {
         const int g = std::atoi(v);
-        c->bs_groups = (g == 1 || g == 4 || g == 5) ? g : 2;
+        c->bs_groups = (g >= 1 && g <= 5) ? g : 0;
     }
     *out = c;
     return MVSV_OK;

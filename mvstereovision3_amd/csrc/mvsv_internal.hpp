@@ -126,7 +126,7 @@ struct mvsv_ctx {
     int cost_res = 1;     // direction passes read the cost residual plane where exact (MVSV_OPT_COST_RESIDUAL)
     int lines_aux = -1;  // L->R line kernel beside the strip kernel: -1 = small launches only, 0 / 1 / 2 force
     int bitslice = 1;    // bit-sliced MODE_HH paths where they apply (MVSV_OPT_BITSLICE, env MVSV_BITSLICE)
-    int bs_groups = 2;   // column groups (3 direction waves each) per bit-sliced strip: 1, 2, 4, 5 (MVSV_BS_GROUPS)
+    int bs_groups = 0;   // column groups (3 direction waves each) per bit-sliced strip: 1-5 (MVSV_BS_GROUPS), 0 = by mode
     int cost_xcd = 1;    // cost kernel: whole row bands per XCD (MVSV_COST_XCD=0: blockIdx order, A/B)
     int bs_fuse = 1;     // bit-sliced batches: R->L lines fused with the WTA (MVSV_BS_FUSE=0: separate, A/B)
     int bs_serial = 0;   // 1: bit-sliced line kernel after the strips on the context stream (MVSV_BS_SERIAL, A/B)

@@ -50,7 +50,7 @@ def test_bitslice_hh_forced(gpu, mvsv, oracle, case, bits, sched):
     assert np.array_equal(got, want), f"bitslice={bits} sched={sched} variant={variant} {kw}: " + report(got, want)
 
 
-@pytest.mark.parametrize("groups", ["1", "2", "4", "5", "2-serial", "2-nofuse", "2-mode0", "1-mode0-nofuse"])
+@pytest.mark.parametrize("groups", ["1", "2", "3", "4", "5", "2-serial", "2-nofuse", "2-mode0", "3-mode0", "1-mode0-nofuse"])
 def test_bitslice_strip_groups(gpu, mvsv, oracle, groups, monkeypatch):
     """Every strip width (column groups per strip) on a 3-frame device batch;
     -serial: the L->R lines after the strips on the context stream instead of
