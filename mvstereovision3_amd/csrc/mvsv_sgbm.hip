@@ -624,24 +624,33 @@ __device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t b, uint32_t 
 
 constexpr int kPath16PF = 12;
 
-template <int NP, bool FIRST, typename AccT, bool NW = false, bool RES = false>
+// LPC lanes per line (2*NP disparities each, D = 2*NP*LPC): 16 (a DPP row),
+// or 8 for D = 16 (captureDisparity's create(0, 16, 5, 200, 800)), eight lines
+// per wave
+template <int LPC>
+constexpr int path16_lines_per_block() { return 4 * (64 / LPC); }
+
+template <int NP, bool FIRST, typename AccT, bool NW = false, bool RES = false, int LPC = 16>
 __device__ __forceinline__ void path16_lines(const void* __restrict__ C, AccT* __restrict__ A,
                                              AccT* __restrict__ dummy, int H, int W1, int D, int dx,
                                              int dy, int P1, int P2, int bx, int f)
 {
+    static_assert(LPC == 8 || LPC == 16, "row-DPP segments of 8 or 16 lanes");
     using AV = AccVec<NP, AccT>;
     using CI = CostIn<NP, RES>;
     constexpr int PF = kPath16PF;
+    constexpr int LPW = 64 / LPC;  // lines per wave
     const int lane = threadIdx.x & 63;
-    const int row = lane >> 4, rl = lane & 15;
+    const int row = lane / LPC, rl = lane % LPC;
     const int nl = num_lines(dx, dy, W1, H);
-    const int line0 = __builtin_amdgcn_readfirstlane((bx * 4 + (int)(threadIdx.x >> 6)) * 4);
+    const int line0 = __builtin_amdgcn_readfirstlane((bx * 4 + (int)(threadIdx.x >> 6)) * LPW);
     if (line0 >= nl) return;
     const int line = min(line0 + row, nl - 1);
     const Line g = line_geometry(line, dx, dy, W1, H);
     const int len = line0 + row < nl ? g.len : 0;
-    const int maxlen = max(max(__builtin_amdgcn_readlane(len, 0), __builtin_amdgcn_readlane(len, 16)),
-                           max(__builtin_amdgcn_readlane(len, 32), __builtin_amdgcn_readlane(len, 48)));
+    int maxlen = __builtin_amdgcn_readlane(len, 0);
+#pragma unroll
+    for (int r = 1; r < LPW; r++) maxlen = max(maxlen, __builtin_amdgcn_readlane(len, r * LPC));
     const size_t frame = (size_t)H * W1 * D;
     const ptrdiff_t step = ((ptrdiff_t)dy * W1 + dx) * D;
     const int d0 = rl * 2 * NP;
@@ -669,8 +678,8 @@ __device__ __forceinline__ void path16_lines(const void* __restrict__ C, AccT* _
         const uint32_t delta2 = sgm_delta2<NW>(minp, P2);
         uint32_t c[NP], ln[NP], o[NP], tt[NP];
         cb[j].get(c);
-        sgm_step_row_t<NP, NW>(lp, delta2, p1x2, c, ln, tt);
-        minp = row_min_i32(lane_min_row<NP>(ln));
+        sgm_step_row_t<NP, NW, LPC>(lp, delta2, p1x2, c, ln, tt);
+        minp = seg_lane_min<LPC>(lane_min_row<NP>(ln));
 #pragma unroll
         for (int p = 0; p < NP; p++) {
             const uint32_t dv = sgm_delta<NW>(tt[p], p2x2);  // delta = t + P2 = P2 - u
@@ -716,14 +725,14 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const void* __restrict
 struct PathDirs {
     int dx[7], dy[7];
 };
-template <int NP, typename AccT, bool NW, bool RES = false>
+template <int NP, typename AccT, bool NW, bool RES = false, int LPC = 16>
 __global__ __launch_bounds__(256) void sgbm_pathdirs16_kernel(const void* __restrict__ C,
                                                               AccT* __restrict__ A, size_t plane,
                                                               AccT* __restrict__ dummy, int H, int W1,
                                                               int D, PathDirs dirs, int P1, int P2)
 {
     const int k = blockIdx.z;
-    path16_lines<NP, true, AccT, NW, RES>(C, acc_add(A, (ptrdiff_t)k * (ptrdiff_t)plane), dummy, H, W1, D,
+    path16_lines<NP, true, AccT, NW, RES, LPC>(C, acc_add(A, (ptrdiff_t)k * (ptrdiff_t)plane), dummy, H, W1, D,
                                           dirs.dx[k], dirs.dy[k], P1, P2, blockIdx.x, blockIdx.y);
 }
 
@@ -1358,6 +1367,7 @@ struct AccRaw<NP, nib2_t> {
 template <int LPR>
 __device__ __forceinline__ int seg_min_i32(int v)
 {
+    if constexpr (LPR == 8) return seg_lane_min<8>(v);
     v = row_min_i32(v);
     if constexpr (LPR == 32) {
         const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
@@ -1374,8 +1384,8 @@ __device__ __forceinline__ void sgm_step_seg_t(const uint32_t (&lp)[NP], uint32_
                                                uint32_t (&ln)[NP], uint32_t (&t)[NP], bool seg_first,
                                                bool seg_last)
 {
-    if constexpr (LPR == 16) {
-        sgm_step_row_t<NP, NW>(lp, delta2, p1x2, c, ln, t);
+    if constexpr (LPR <= 16) {
+        sgm_step_row_t<NP, NW, LPR>(lp, delta2, p1x2, c, ln, t);
     } else {
         const uint32_t MAXP = 0x7fff7fffu;
         // zero-filled wave shifts (bound_ctrl) OR'ed with MAX at the segment
@@ -1476,7 +1486,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     // into scratch (round 6 dispatch census, tests/test_kernel_scratch.py).
     // The step loop is unrolled by LPR, so PF must divide it.
     constexpr int kF32Words = (RESF ? 1 : NP) + NACC * AccRaw<NP, AccT>::NW;
-    constexpr int PF = LPR == 32 ? (kF32Words > 10 ? 4 : MVSV_FINAL32_PF) : final16_pf<NP, NACC, AccT, UQ>();
+    constexpr int PF = LPR == 32 ? (kF32Words > 10 ? 4 : MVSV_FINAL32_PF)
+                                 : (final16_pf<NP, NACC, AccT, UQ>() < LPR ? final16_pf<NP, NACC, AccT, UQ>() : LPR);
     static_assert(LPR % PF == 0, "prefetch slots must divide the unrolled step loop");
     constexpr int RPW = 64 / LPR;     // image rows per wave
     constexpr int DR = 2 * NP * LPR;  // disparities of a row (D)
@@ -1957,16 +1968,17 @@ __global__ void fill_s16_kernel(int16_t* __restrict__ out, size_t os, size_t ofs
 }
 
 // sheared-strip schedule: enabled, and int32 element offsets cover a frame
-template <int NP, int NACC, typename AccT, bool NW = false, bool RES = false>
+template <int NP, int NACC, typename AccT, bool NW = false, bool RES = false, int LPC = 16>
 void launch_final16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const int16_t* Cv,
                     const AccT* Av, size_t plane, int16_t* raw, const void* Rv = nullptr,
                     const uint16_t* Mv = nullptr)
 {
-    // NP: disparity pairs per lane at 16 lanes per row.  D >= 128: 32 lanes per
-    // row (half the pairs per lane, twice the rows in flight per SIMD); a lane
-    // keeps >= 2 pairs, so it reads whole 4-disparity nibble groups.
-    constexpr int LPR = NP >= 4 ? MVSV_FINAL_LPR : 16;
-    constexpr int NPL = NP * 16 / LPR;
+    // NP: disparity pairs per lane at LPC lanes per row (LPC = 8: D = 16, eight
+    // rows per wave).  D >= 128: 32 lanes per row (half the pairs per lane,
+    // twice the rows in flight per SIMD); a lane keeps >= 2 pairs, so it reads
+    // whole 4-disparity nibble groups.
+    constexpr int LPR = LPC == 8 ? 8 : (NP >= 4 ? MVSV_FINAL_LPR : 16);
+    constexpr int NPL = LPC == 8 ? NP : NP * 16 / LPR;
     constexpr int RPW = 64 / LPR;
     const dim3 grid((H + RPW - 1) / RPW, n);
     uint32_t* keys = (uint32_t*)ctx->keys.ptr;
@@ -2019,6 +2031,7 @@ static bool use_strips(const mvsv_ctx* ctx, const SgbmEff& e, int H)
 // ctx->path_sched: 0 = by launch size, 1 / 2 force (tests, A/B).
 static int path_schedule(const mvsv_ctx* ctx, const SgbmEff& e, int H, int n)
 {
+    if (e.D == 16 && ctx->path16 && ctx->path_sched != 1) return 2;  // launch_paths_d16
     if (!ctx->path16 || !(e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256)) return 0;
     const bool dirs_ok = e.P2 <= 15 || ctx->path_sched == 2;  // nibble planes; wider planes when forced
     if (ctx->path_sched == 2) return 2;
@@ -2339,7 +2352,7 @@ int launch_paths(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* 
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels");
 }
 
-template <int NP, typename AccT, bool NW, bool RES = false>
+template <int NP, typename AccT, bool NW, bool RES = false, int LPC = 16>
 int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, const void* Cin,
                       AccT* Av, int16_t* raw, const uint16_t* Mv = nullptr)
 {
@@ -2356,15 +2369,16 @@ int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int1
     const size_t plane = (size_t)n * H * e.W1 * e.D;
     {
         StageTimer tm(ctx, kStagePath);
-        hipLaunchKernelGGL((sgbm_pathdirs16_kernel<NP, AccT, NW, RES>), dim3((maxnl + 15) / 16, n, ndir), dim3(256),
-                           0, ctx->stream, Cin, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, pd, e.P1,
-                           e.P2);
+        constexpr int lpb = path16_lines_per_block<LPC>();
+        hipLaunchKernelGGL((sgbm_pathdirs16_kernel<NP, AccT, NW, RES, LPC>), dim3((maxnl + lpb - 1) / lpb, n, ndir),
+                           dim3(256), 0, ctx->stream, Cin, Av, plane, (AccT*)ctx->dummy.ptr, H, e.W1, e.D, pd,
+                           e.P1, e.P2);
     }
     StageTimer tm(ctx, kStageFinal);
     if (ndir == 7)
-        launch_final16<NP, 7, AccT, NW, RES>(ctx, n, H, W, e, Cv, Av, plane, raw, Cin, Mv);
+        launch_final16<NP, 7, AccT, NW, RES, LPC>(ctx, n, H, W, e, Cv, Av, plane, raw, Cin, Mv);
     else
-        launch_final16<NP, 4, AccT, NW, RES>(ctx, n, H, W, e, Cv, Av, plane, raw, Cin, Mv);
+        launch_final16<NP, 4, AccT, NW, RES, LPC>(ctx, n, H, W, e, Cv, Av, plane, raw, Cin, Mv);
     return check_hip(ctx, hipGetLastError(), "sgbm path kernels (directions side by side)");
 }
 
@@ -2406,6 +2420,26 @@ int launch_paths16_acc(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int
     }
     if (acc_is_u8(e)) return launch_paths16<NP, uint8_t>(ctx, n, H, W, e, Cv, (uint8_t*)Av, raw);
     return launch_paths16<NP, uint16_t>(ctx, n, H, W, e, Cv, (uint16_t*)Av, raw);
+}
+
+// D = 16 (captureDisparity's create(0, 16, 5, 200, 800)): the directions side
+// by side at 8 lanes per line / row (one disparity pair per lane), in every
+// launch shape -- the per-pixel work is small enough that the planes' traffic
+// never outweighs the single-frame latency of a strip chain.  Planes as in
+// launch_paths16_acc's side-by-side branch: nibbles (P2 <= 15), else bytes or
+// u16.
+int launch_paths_d16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16_t* Cv, void* Av,
+                     int16_t* raw)
+{
+    int rc;
+    if ((rc = ensure(ctx, ctx->dummy, 512 * 16 * 2, "sgbm dummy slots"))) return rc;
+    if ((rc = ensure(ctx, ctx->keys, (size_t)n * H * W * 4, "sgbm right-view keys"))) return rc;
+    if (e.P2 <= 15) {
+        if (sgbm_no_wrap(e)) return launch_paths_dirs<1, nib2_t, true, false, 8>(ctx, n, H, W, e, Cv, Cv, (nib2_t*)Av, raw);
+        return launch_paths_dirs<1, nib2_t, false, false, 8>(ctx, n, H, W, e, Cv, Cv, (nib2_t*)Av, raw);
+    }
+    if (acc_is_u8(e)) return launch_paths_dirs<1, uint8_t, false, false, 8>(ctx, n, H, W, e, Cv, Cv, (uint8_t*)Av, raw);
+    return launch_paths_dirs<1, uint16_t, false, false, 8>(ctx, n, H, W, e, Cv, Cv, (uint16_t*)Av, raw);
 }
 
 template <int NP>
@@ -2549,6 +2583,8 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     const bool wide = ctx->path16 && (e.D == 32 || e.D == 64 || e.D == 128 || e.D == 256);
     if (Bv) {
         rc = bsgm_paths(ctx, n, H, W, e, Cv, Bv, Mv, raw, sched == 2);
+    } else if (e.D == 16 && sched == 2) {
+        rc = launch_paths_d16(ctx, n, H, W, e, Cv, Sv, raw);
     } else if (wide) {
         switch (e.D) {
         case 32: rc = launch_paths16_acc<1>(ctx, n, H, W, e, Cv, Rv, Mv, Sv, raw); break;
