@@ -2053,6 +2053,17 @@ static int path_schedule(const mvsv_ctx* ctx, const SgbmEff& e, int H, int n)
         // lose (1.87 -> 1.95 ms: seven planes into the final kernel)
         if (2 * blocks <= ctx->cus) return 2;
     }
+    if (ctx->path_sched == 0 && e.P2 > 15) {
+        // byte / u16 planes (liveDisparity's create(0, 64, 9, 648, 2592)): side by
+        // side while the planes stay small -- their bytes against the strip
+        // chain's latency.  Measured (1280x960, MI355X r06 s2a / d16a): MODE_SGBM
+        // D 32 x 1-3 frames 0.91 -> 0.53, 1.20 -> 1.07 ms; D 64 x 1, 2 frames
+        // 1.16 -> 0.71, 1.34 -> 1.12 ms, x 4 1.98 -> 2.14 (strips kept); D 128 x 1
+        // 1.50 -> 1.08, x 2 1.86 -> 1.90; D 256 x 1 2.08 -> 2.16; MODE_HH D 64 x 1
+        // 1.18 -> 0.90, x 2 1.52 -> 1.59
+        const double bytes = (double)n * e.W1 * H * e.D * (e.fullDP ? 7 : 4) * (acc_is_u8(e) ? 1 : 2);
+        if (bytes <= 1.4e9) return 2;
+    }
     return use_strips(ctx, e, H) ? 1 : 0;
 }
 
