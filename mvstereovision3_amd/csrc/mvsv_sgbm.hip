@@ -1414,7 +1414,9 @@ template <int NP, int NACC, typename AccT, bool UQ>
 constexpr int final16_pf()
 {
     constexpr int words = NP + NACC * AccRaw<NP, AccT>::NW;  // VGPRs per step
-    constexpr int budget = UQ ? 96 : 160;
+    // three or more planes (MODE_HH, side by side) unpack more per step: at
+    // 160 buffer VGPRs those instances spilled 36-105 VGPRs (round 6 audit)
+    constexpr int budget = UQ ? 96 : (NACC >= 3 ? 80 : 160);
     return budget / words >= 16 ? 16 : (budget / words >= 8 ? 8 : 4);
 }
 
@@ -1486,7 +1488,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NP >= 8 ? 1 
     // into scratch (round 6 dispatch census, tests/test_kernel_scratch.py).
     // The step loop is unrolled by LPR, so PF must divide it.
     constexpr int kF32Words = (RESF ? 1 : NP) + NACC * AccRaw<NP, AccT>::NW;
-    constexpr int PF = LPR == 32 ? (kF32Words > 10 ? 4 : MVSV_FINAL32_PF)
+    constexpr int PF = LPR == 32 ? (kF32Words > 24 ? 2 : kF32Words > 10 ? 4 : MVSV_FINAL32_PF)
                                  : (final16_pf<NP, NACC, AccT, UQ>() < LPR ? final16_pf<NP, NACC, AccT, UQ>() : LPR);
     static_assert(LPR % PF == 0, "prefetch slots must divide the unrolled step loop");
     constexpr int RPW = 64 / LPR;     // image rows per wave
