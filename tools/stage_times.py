@@ -2,6 +2,7 @@
 
 Usage (on the GPU box): python tools/stage_times.py [--frames F] [--width W --height H]
     [--ndisp D] [--mode 0|1] [--p1 P1 --p2 P2 --bs BS] [--steps K]
+    [--speckle-window N --speckle-range R]
 Defaults: config 5 (liveDisparity: create(0, 256, 9, 648, 2592), MODE_SGBM, one
 1280x960 frame).  Env knobs (MVSV_PATH_SCHEDULE, MVSV_STRIP_WAVES, ...) apply."""
 import argparse
@@ -25,12 +26,14 @@ def main():
     ap.add_argument("--p2", type=int, default=2592)
     ap.add_argument("--mode", type=int, default=0)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--speckle-window", type=int, default=0)
+    ap.add_argument("--speckle-range", type=int, default=0)
     a = ap.parse_args()
     import numpy as np
     import torch
     import mvstereovision3_amd as mvsv
     from mvstereovision3_amd import _lib
-    m = mvsv.StereoSGBM.create(a.mind, a.ndisp, a.bs, a.p1, a.p2)
+    m = mvsv.StereoSGBM.create(a.mind, a.ndisp, a.bs, a.p1, a.p2, 0, 0, 0, a.speckle_window, a.speckle_range)
     m.setMode(a.mode)
     host = [mvsv.synth_pair(0x5EED0000 + i, a.width, a.height, a.mind, a.ndisp) for i in range(a.frames)]
     L = torch.from_numpy(np.stack([h[0] for h in host])).cuda()
