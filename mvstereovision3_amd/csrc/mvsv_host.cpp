@@ -366,6 +366,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
     if (const char* v = std::getenv("MVSV_COST_TY")) c->cost_ty = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("MVSV_PATH_SCHEDULE")) c->path_sched = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("MVSV_STRIP_WAVES")) c->strip_waves = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("MVSV_TRI32")) c->tri32 = std::atoi(v) != 0;
     if (const char* v = std::getenv("MVSV_COST_RESIDUAL")) c->cost_res = std::atoi(v) != 0;
     if (const char* v = std::getenv("MVSV_BM_TY")) c->bm_ty = std::max(0, std::min(128, std::atoi(v)));
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess) {

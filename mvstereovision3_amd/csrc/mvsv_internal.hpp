@@ -122,6 +122,8 @@ struct mvsv_ctx {
     int cost_ty = 0;  // cost-volume tile height (0 = by image height); MVSV_COST_TY for A/B runs
     int tri = 1;     // sheared-strip kernels: three directions per sweep
     int path_sched = 0;   // 16-lane path schedule: 0 = by launch size, 1 = strips, 2 = directions side by side
+    int tri32 = 1;
+    int tri_xseg = 0;     // A/B: one strip chain's neighbours on one XCD (MVSV_TRI_XSEG)        // D = 256 narrow strips on 32 lanes per column (MVSV_TRI32)
     int strip_waves = 0;  // compute waves per strip (0 = by launch size; 4 or the wide count forces)
     int cost_res = 1;     // direction passes read the cost residual plane where exact (MVSV_OPT_COST_RESIDUAL)
     int lines_aux = -1;  // L->R line kernel beside the strip kernel: -1 = small launches only, 0 / 1 / 2 force

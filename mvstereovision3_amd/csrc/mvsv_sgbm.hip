@@ -592,6 +592,51 @@ __device__ __forceinline__ int seg_lane_min(int v)
     return v;
 }
 
+// Lane segments of the final kernel: LPR lanes own one image row (16: a DPP
+// row; 32: two DPP rows joined by v_permlane16_swap).
+template <int LPR>
+__device__ __forceinline__ int seg_min_i32(int v)
+{
+    if constexpr (LPR == 8) return seg_lane_min<8>(v);
+    v = row_min_i32(v);
+    if constexpr (LPR == 32) {
+        const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+        v = min((int)sw[0], (int)sw[1]);
+    }
+    return v;
+}
+// sgm_step_row_t over an LPR-lane segment: the d-1 / d+1 neighbours of a lane's
+// first / last pair come from the adjacent lane of the segment (MAX at the
+// segment ends).
+template <int NP, int LPR, bool NW>
+__device__ __forceinline__ void sgm_step_seg_t(const uint32_t (&lp)[NP], uint32_t delta2,
+                                               uint32_t p1x2, const uint32_t (&c)[NP],
+                                               uint32_t (&ln)[NP], uint32_t (&t)[NP], bool seg_first,
+                                               bool seg_last)
+{
+    if constexpr (LPR <= 16) {
+        sgm_step_row_t<NP, NW, LPR>(lp, delta2, p1x2, c, ln, t);
+    } else {
+        const uint32_t MAXP = 0x7fff7fffu;
+        // zero-filled wave shifts (bound_ctrl) OR'ed with MAX at the segment
+        // ends (L values are in [0, 0x7fff], so x | MAXP == MAXP): one
+        // v_or_b32_dpp per neighbour
+        const uint32_t prev_hi =
+            (uint32_t)__builtin_amdgcn_mov_dpp((int)lp[NP - 1], 0x138, 0xf, 0xf, true) | (seg_first ? MAXP : 0u);
+        const uint32_t next_lo =
+            (uint32_t)__builtin_amdgcn_mov_dpp((int)lp[0], 0x130, 0xf, 0xf, true) | (seg_last ? MAXP : 0u);
+        uint32_t X[NP + 1];  // X[q + 1] = X_q, X[0] = X_{-1}
+        X[0] = pk_min(prev_hi, lp[0]);
+#pragma unroll
+        for (int q = 0; q + 1 < NP; q++) X[q + 1] = pk_min(lp[q], lp[q + 1]);
+        X[NP] = pk_min(lp[NP - 1], next_lo);
+#pragma unroll
+        for (int p = 0; p < NP; p++)
+            sgm_pair<NW>(lp[p], __builtin_amdgcn_alignbit(X[p + 1], X[p], 16), delta2, p1x2, c[p], ln[p],
+                         t[p]);
+    }
+}
+
 // The lane's minimum over its NP pairs in BOTH halves (the swap is a VOP3P
 // op_sel, no extra instruction): for L in [0, 0x7fff] the packed (m, m) orders
 // like m as an int32, so the segment butterfly runs on it unchanged and the
@@ -764,16 +809,22 @@ __global__ __launch_bounds__(256) void sgbm_pathdirs16_kernel(const void* __rest
 // per-column minimum is a 3-step butterfly, and the lane-boundary neighbours,
 // the step's row minima and its bookkeeping are shared by twice the work --
 // the throughput shape for D = 128 batches, two 512-thread blocks per CU).
+// LPC = 32 (round 6, D = 256 launches too small for wide strips: config 5's
+// one or two frames): two DPP rows per U-column, 4 disparity pairs per lane --
+// half the per-wave work of a strip step at the same strip width (8 compute
+// waves x 2 columns); the three boundary items then need 96 exchange lanes,
+// so such a block has two exchange waves.
 template <int NP, int LPC = 16>
 constexpr int tri_wide_waves() { return LPC == 8 ? 7 : (NP >= 8 ? 7 : 15); }
 template <int NP, int LPC = 16>
-constexpr int tri_narrow_waves() { return LPC == 8 ? 4 : (NP >= 8 ? 4 : 8); }
+constexpr int tri_narrow_waves() { return LPC == 8 ? 4 : LPC == 32 ? 8 : (NP >= 8 ? 4 : 8); }
 template <int NP, int WV, int LPC = 16>
 struct TriCfg {
     static constexpr int kWaves = WV;
     static constexpr int kCPW = 64 / LPC;   // U-columns per compute wave
     static constexpr int kSW = kCPW * kWaves;  // U-columns per strip
-    static constexpr int kThreads = 64 * (kWaves + 1);
+    static constexpr int kComm = LPC == 32 ? 2 : 1;  // exchange waves: 3 items x LPC lanes
+    static constexpr int kThreads = 64 * (kWaves + kComm);
     // blocks per CU the register budget aims at: one 1024-thread block, or two
     // 512-thread ones (4 waves per SIMD either way); D = 256 on 16 lanes: 2.
     // (Narrow strips reading the cost residual aim at 5: two 9-wave blocks
@@ -885,7 +936,9 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU + (RES && WV
     int* lmin = (int*)(lds + TL::kLDw);
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool comm = w == kTriWaves;
+    const bool comm = w >= kTriWaves;
+    const int cw = comm ? w - kTriWaves : 0;  // exchange wave rank (LPC = 32: 0 or 1)
+    const bool comm0 = comm && cw == 0;     // the one that records statistics / traces
     const int r = lane / LPC, rl = lane % LPC;
     // strips counted from the right; pass 0 sweeps down (sy = +1), pass 1 up
     // (sy = -1), each into its own accumulator plane; every strip's producer
@@ -951,8 +1004,9 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU + (RES && WV
     // unpredicated and its wait counts are exact.  A step's granules are laid
     // out [granule i][item row][lane]: each of the NG store / load
     // instructions covers 512 contiguous bytes.
-    const int jj = min(r, 2);
-    const bool jlive = r < 3;
+    const int ir = cw * (64 / LPC) + r;  // item row of this exchange lane
+    const int jj = min(ir, 2);
+    const bool jlive = ir < 3;
     const int bcol = kTriSW + (jj == 2 ? 1 : 0);  // LDS column the consumed item lands in
     const int bdir = jj == 0 ? 0 : 1;
     const int pcol = jj == 2 ? 1 : 0;              // own column published as item jj
@@ -1031,7 +1085,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU + (RES && WV
         unsigned long long* q = pdst + (size_t)clampi(t, 0, H - 1) * bstep;
 #pragma unroll
         for (int i = 0; i < NG; i++) __hip_atomic_store(q + 4 * LPC * i, g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (trace_h && lane == 0)  // MVSV_TRI_TRACE: when step t went out (100 MHz clock)
+        if (trace_h && comm0 && lane == 0)  // MVSV_TRI_TRACE: when step t went out (100 MHz clock)
             stats[(size_t)bx * (8 + 2 * trace_h) + 8 + t] = __builtin_amdgcn_s_memrealtime();
     };
 
@@ -1074,7 +1128,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU + (RES && WV
         const int cur = i & 1, prv = cur ^ 1;
         if (i > 0) publish(t - 1, prv);
         bconsume(t, cur, bg[j % BF]);
-        if (trace_h && lane == 0)  // when the producer's step t was in
+        if (trace_h && comm0 && lane == 0)  // when the producer's step t was in
             stats[(size_t)bx * (8 + 2 * trace_h) + 8 + trace_h + t] = __builtin_amdgcn_s_memrealtime();
         bload(t + BF, bg[j % BF]);
         __syncthreads();
@@ -1096,10 +1150,19 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU + (RES && WV
         // the column minimum of one direction (packed (m, m) in the no-wrap
         // form) and the next step's delta from it
         auto dmin = [&](const uint32_t (&n)[NP]) -> int {
-            if constexpr (NW)
+            if constexpr (LPC == 32)
+                return seg_min_i32<32>(NW ? (int)lane_min_pk<NP>(n) : lane_min_row<NP>(n));
+            else if constexpr (NW)
                 return seg_lane_min<LPC>((int)lane_min_pk<NP>(n));
             else
                 return seg_lane_min<LPC>(lane_min_row<NP>(n));
+        };
+        // one recurrence step over the column's LPC lanes
+        auto rstep = [&](const uint32_t (&lp)[NP], uint32_t delta2, uint32_t (&n)[NP], uint32_t (&u)[NP]) {
+            if constexpr (LPC == 32)
+                sgm_step_seg_t<NP, 32, NW>(lp, delta2, p1x2, c, n, u, rl == 0, rl == LPC - 1);
+            else
+                sgm_step_row_t<NP, NW, LPC>(lp, delta2, p1x2, c, n, u);
         };
         auto dl2 = [&](int m) -> uint32_t {
             if constexpr (NW)
@@ -1115,7 +1178,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU + (RES && WV
 #if MVSV_TRI_STEP_SEQ
         {  // (1, sy): the strip's own column, state in registers
             uint32_t n[NP], u[NP];
-            sgm_step_row_t<NP, NW, LPC>(la, dl2(ma), p1x2, c, n, u);
+            rstep(la, dl2(ma), n, u);
 #pragma unroll
             for (int p = 0; p < NP; p++) o[p] = acc(p2x3, u[p]);
             const int mn = dmin(n);
@@ -1135,7 +1198,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU + (RES && WV
             for (int p = 0; p < NP; p++) pv[p] = src[p * LPC];
             const int mp = *mcol(prv, dir, col + 1 + dir);
             uint32_t n[NP], u[NP];
-            sgm_step_row_t<NP, NW, LPC>(pv, dl2(mp), p1x2, c, n, u);
+            rstep(pv, dl2(mp), n, u);
 #pragma unroll
             for (int p = 0; p < NP; p++) o[p] = acc(o[p], u[p]);
             const int mn = dmin(n);
@@ -1163,9 +1226,9 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU + (RES && WV
         }
         const int mb = *mcol(prv, 0, col + 1), mc = *mcol(prv, 1, col + 2);
         uint32_t na[NP], nb[NP], nc[NP], ta[NP], tb_[NP], tc[NP];
-        sgm_step_row_t<NP, NW, LPC>(la, dl2(ma), p1x2, c, na, ta);
-        sgm_step_row_t<NP, NW, LPC>(pb, dl2(mb), p1x2, c, nb, tb_);
-        sgm_step_row_t<NP, NW, LPC>(pc, dl2(mc), p1x2, c, nc, tc);
+        rstep(la, dl2(ma), na, ta);
+        rstep(pb, dl2(mb), nb, tb_);
+        rstep(pc, dl2(mc), nc, tc);
         const int mna = dmin(na), mnb = dmin(nb), mnc = dmin(nc);
 #pragma unroll
         for (int p = 0; p < NP; p++) o[p] = acc(acc(acc(p2x3, ta[p]), tb_[p]), tc[p]);
@@ -1218,7 +1281,7 @@ __attribute__((amdgpu_waves_per_eu(TriCfg<NP, WV, LPC>::kWavesPerEU + (RES && WV
     }
     if (comm) {
         publish(te - 1, (len - 1) & 1);
-        if (stats && lane == 0) {
+        if (stats && comm0 && lane == 0) {
             unsigned long long* q = stats + (size_t)bx * (8 + 2 * trace_h);
             q[0] = st_t0;
             q[1] = __builtin_amdgcn_s_memtime();
@@ -1361,51 +1424,6 @@ struct AccRaw<NP, nib2_t> {
         }
     }
 };
-
-// Lane segments of the final kernel: LPR lanes own one image row (16: a DPP
-// row; 32: two DPP rows joined by v_permlane16_swap).
-template <int LPR>
-__device__ __forceinline__ int seg_min_i32(int v)
-{
-    if constexpr (LPR == 8) return seg_lane_min<8>(v);
-    v = row_min_i32(v);
-    if constexpr (LPR == 32) {
-        const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
-        v = min((int)sw[0], (int)sw[1]);
-    }
-    return v;
-}
-// sgm_step_row_t over an LPR-lane segment: the d-1 / d+1 neighbours of a lane's
-// first / last pair come from the adjacent lane of the segment (MAX at the
-// segment ends).
-template <int NP, int LPR, bool NW>
-__device__ __forceinline__ void sgm_step_seg_t(const uint32_t (&lp)[NP], uint32_t delta2,
-                                               uint32_t p1x2, const uint32_t (&c)[NP],
-                                               uint32_t (&ln)[NP], uint32_t (&t)[NP], bool seg_first,
-                                               bool seg_last)
-{
-    if constexpr (LPR <= 16) {
-        sgm_step_row_t<NP, NW, LPR>(lp, delta2, p1x2, c, ln, t);
-    } else {
-        const uint32_t MAXP = 0x7fff7fffu;
-        // zero-filled wave shifts (bound_ctrl) OR'ed with MAX at the segment
-        // ends (L values are in [0, 0x7fff], so x | MAXP == MAXP): one
-        // v_or_b32_dpp per neighbour
-        const uint32_t prev_hi =
-            (uint32_t)__builtin_amdgcn_mov_dpp((int)lp[NP - 1], 0x138, 0xf, 0xf, true) | (seg_first ? MAXP : 0u);
-        const uint32_t next_lo =
-            (uint32_t)__builtin_amdgcn_mov_dpp((int)lp[0], 0x130, 0xf, 0xf, true) | (seg_last ? MAXP : 0u);
-        uint32_t X[NP + 1];  // X[q + 1] = X_q, X[0] = X_{-1}
-        X[0] = pk_min(prev_hi, lp[0]);
-#pragma unroll
-        for (int q = 0; q + 1 < NP; q++) X[q + 1] = pk_min(lp[q], lp[q + 1]);
-        X[NP] = pk_min(lp[NP - 1], next_lo);
-#pragma unroll
-        for (int p = 0; p < NP; p++)
-            sgm_pair<NW>(lp[p], __builtin_amdgcn_alignbit(X[p + 1], X[p], 16), delta2, p1x2, c[p], ln[p],
-                         t[p]);
-    }
-}
 
 // Steps of C / accumulator prefetch: as deep as ~160 VGPRs of buffers allow
 // (a power of two dividing the 16-step flush period).  The kernel is bound by
@@ -2200,6 +2218,15 @@ template <int NP, typename AccT, bool NW, bool RES>
 int launch_tri(mvsv_ctx* ctx, int n, int H, const SgbmEff& e, const void* Cv, AccT* Av, size_t plane,
                int npass)
 {
+    if constexpr (NP == 8 && !RES) {
+        // D = 256 launches that would run narrow strips (one or two frames):
+        // 32 lanes per column (MVSV_TRI32 = 0: the 16-lane narrow strips)
+        constexpr int wide = tri_wide_waves<NP, 16>();
+        const long long blocks = (long long)npass * n * ((e.W1 + H - 1 + 4 * wide - 1) / (4 * wide));
+        if (ctx->tri32 && ctx->strip_waves == 0 && blocks < ctx->cus)
+            return launch_tri_wv<NP / 2, tri_narrow_waves<NP / 2, 32>(), 32, AccT, NW, RES>(ctx, n, H, e, Cv, Av,
+                                                                                           plane, npass);
+    }
     return launch_tri_lpc<NP, 16, AccT, NW, RES>(ctx, n, H, e, Cv, Av, plane, npass);
 }
 
