@@ -108,8 +108,8 @@ def main():
 
     for i in range(a.large):  # batch shapes: wide strips, lines after the strips
         W, H = (640, 480) if rng.integers(0, 3) else (1280, 960)
-        n = int(rng.choice([4, 8])) if W == 640 else int(rng.choice([2, 4]))
-        D = int(rng.choice([64, 128, 256]))
+        n = int(rng.choice([1, 4, 8])) if W == 640 else int(rng.choice([1, 2, 4]))
+        D = int(rng.choice([16, 64, 128, 256]))  # round 6: D 16 (captureDisparity), one-frame launches
         kw = dict(minDisparity=int(rng.integers(-4, 4)), numDisparities=D,
                   blockSize=int(rng.choice([3, 5, 9, 13])), P1=int(rng.choice([0, 2, 8, 648])),
                   P2=int(rng.choice([0, 5, 32, 2592])), disp12MaxDiff=int(rng.integers(-1, 3)),
