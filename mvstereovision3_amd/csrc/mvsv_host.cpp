@@ -367,6 +367,7 @@ int mvsv_create(mvsv_ctx** out, int hip_device)
     if (const char* v = std::getenv("MVSV_PATH_SCHEDULE")) c->path_sched = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("MVSV_STRIP_WAVES")) c->strip_waves = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("MVSV_TRI32")) c->tri32 = std::atoi(v) != 0;
+    if (const char* v = std::getenv("MVSV_FINAL_SPLIT")) c->final_split = std::atoi(v) != 0;
     if (const char* v = std::getenv("MVSV_COST_RESIDUAL")) c->cost_res = std::atoi(v) != 0;
     if (const char* v = std::getenv("MVSV_BM_TY")) c->bm_ty = std::max(0, std::min(128, std::atoi(v)));
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess) {
@@ -586,6 +587,13 @@ size_t mvsv_sgbm_workspace_bytes(int n, int W, int H, const mvsv_sgbm_params* p)
         if (side > acc) b += side - acc;
         const size_t nstrips = ((size_t)e.W1 + H - 1 + 63) / 64;
         b += 2 * (size_t)n * nstrips * H * 36 * 8;
+    } else if (e.P2 > 15 && e.W1 > 0) {
+        // directions side by side on byte / u16 planes (round 6: the reference's
+        // liveDisparity / captureDisparity shapes), one plane per direction
+        // (D <= 32: R->L included), beyond the one-volume accumulator budget above
+        const size_t planes = (e.fullDP ? 7 : 4) + (e.D <= 32 ? 1 : 0), ebytes = (e.fullDP ? 8 : 5) * e.P2 <= 255 ? 1 : 2;
+        const size_t side = (size_t)n * e.W1 * H * e.D * planes * ebytes, acc = (size_t)n * vol;
+        if (side > acc) b += side - acc;
     }
     return b;
 }

@@ -123,6 +123,7 @@ struct mvsv_ctx {
     int tri = 1;     // sheared-strip kernels: three directions per sweep
     int path_sched = 0;   // 16-lane path schedule: 0 = by launch size, 1 = strips, 2 = directions side by side
     int tri32 = 1;
+    int final_split = 1;  // side by side on byte / u16 planes: R->L as a chain set + per-pixel WTA (MVSV_FINAL_SPLIT)
     int tri_xseg = 0;     // A/B: one strip chain's neighbours on one XCD (MVSV_TRI_XSEG)        // D = 256 narrow strips on 32 lanes per column (MVSV_TRI32)
     int strip_waves = 0;  // compute waves per strip (0 = by launch size; 4 or the wide count forces)
     int cost_res = 1;     // direction passes read the cost residual plane where exact (MVSV_OPT_COST_RESIDUAL)

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "mvsv_cost_layout.hpp"
@@ -768,7 +769,7 @@ __global__ __launch_bounds__(256) void sgbm_path16_kernel(const void* __restrict
 // instead of as sheared strips, whose 480-step chain is the single-frame
 // critical path.
 struct PathDirs {
-    int dx[7], dy[7];
+    int dx[8], dy[8];
 };
 template <int NP, typename AccT, bool NW, bool RES = false, int LPC = 16>
 __global__ __launch_bounds__(256) void sgbm_pathdirs16_kernel(const void* __restrict__ C,
@@ -1979,6 +1980,154 @@ __global__ __launch_bounds__(64) void sgbm_final_kernel(const int16_t* __restric
     }
 }
 
+// ---------------------------------------------------------------------------
+// 5b. WTA of the split side-by-side form (round 6): the R->L direction ran as
+// one more side-by-side chain set, so every pixel's S is a sum of planes --
+// S = min(ndir (C - P2) + sum of the ndir deltas, MAX_COST), exact in int32 --
+// and the WTA, uniqueness ratio, sub-pixel fit and right-view keys run on a
+// thread per pixel with no chain along the row; a row's block then runs the
+// left-right check (as sgbm_final16_kernel).  Byte / u16 planes, element order
+// d within a pixel.
+// ---------------------------------------------------------------------------
+constexpr int kWtaThreads = 256;
+
+template <typename AccT>
+__device__ __forceinline__ void load8_planes(const AccT* p, uint32_t (&v)[8])
+{
+    if constexpr (sizeof(AccT) == 2) {
+        const uint4 t = *(const uint4*)p;
+        const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            v[2 * i] = w[i] & 0xffffu;
+            v[2 * i + 1] = w[i] >> 16;
+        }
+    } else {
+        const uint2 t = *(const uint2*)p;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            v[i] = (t.x >> (8 * i)) & 0xffu;
+            v[4 + i] = (t.y >> (8 * i)) & 0xffu;
+        }
+    }
+}
+
+// LPP = D / 8 lanes per pixel, 8 disparities per lane (coalesced 16-byte
+// loads of C and of every plane); the lanes of a pixel reduce the key, the
+// uniqueness minimum and S(best -+ 1) with lane shuffles, and the pixel's first
+// lane finishes it.
+template <typename AccT, bool UQ, int LPP>
+__global__ __launch_bounds__(kWtaThreads) void sgbm_wta_planes_kernel(const int16_t* __restrict__ C,
+                                                                     const AccT* __restrict__ A, size_t plane,
+                                                                     int nplanes, int H, int W, SgbmEff e,
+                                                                     int16_t* __restrict__ raw,
+                                                                     uint32_t* __restrict__ keys)
+{
+    static_assert(LPP >= 2 && LPP <= 32 && (LPP & (LPP - 1)) == 0, "8 disparities per lane, D = 16 .. 256");
+    constexpr int PPB = kWtaThreads / LPP;  // pixels per block iteration
+    const int y = blockIdx.x, f = blockIdx.y;
+    const int D = 8 * LPP, W1 = e.W1, INV = e.invalid, minD = e.minD, minX1 = e.minX1;
+    int16_t* orow = raw + ((size_t)f * H + y) * W;
+    uint32_t* krow = keys + ((size_t)f * H + y) * W;
+    for (int x = threadIdx.x; x < W; x += kWtaThreads) {
+        orow[x] = (int16_t)INV;
+        krow[x] = 0xffffffffu;
+    }
+    __threadfence_block();
+    __syncthreads();
+    const bool lane_rule = !e.fullDP && !(e.variant & MVSV_VARIANT_WTA_MIN_D);
+    const int ndir = e.fullDP ? 8 : 5;
+    const size_t row0 = ((size_t)f * H + y) * W1;
+    const int sl = threadIdx.x % LPP, gbase = (int)(threadIdx.x & 63) - sl;  // lane in the pixel, its first lane
+    const int d0 = 8 * sl;
+    for (int xb = 0; xb < W1; xb += PPB) {
+        const int xr = xb + (int)threadIdx.x / LPP;
+        const int x = min(xr, W1 - 1);
+        const size_t off = (row0 + x) * D + d0;
+        int S[8];
+        {
+            const uint4 cw = *(const uint4*)(C + off);
+            const uint32_t cv[4] = {cw.x, cw.y, cw.z, cw.w};
+            int acc[8];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                acc[2 * i] = ndir * ((int)(cv[i] & 0xffffu) - e.P2);
+                acc[2 * i + 1] = ndir * ((int)(cv[i] >> 16) - e.P2);
+            }
+            for (int k = 0; k < nplanes; k++) {
+                uint32_t dv[8];
+                load8_planes<AccT>(A + (size_t)k * plane + off, dv);
+#pragma unroll
+                for (int i = 0; i < 8; i++) acc[i] += (int)dv[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) S[i] = min(acc[i], kMaxCost);
+        }
+        // argmin, ties in OpenCV's order (d, or MODE_SGBM's SIMD lane d mod 8 first)
+        uint32_t key = 0xffffffffu;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int d = d0 + i;
+            const uint32_t sub = lane_rule ? (uint32_t)((i << 12) | (d >> 3)) : (uint32_t)d;
+            key = min(key, ((uint32_t)S[i] << 16) | sub);
+        }
+#pragma unroll
+        for (int m = 1; m < LPP; m <<= 1) key = min(key, (uint32_t)__shfl_xor((int)key, m, 64));
+        const int minS = (int)(key >> 16), sub = (int)(key & 0xffffu);
+        const int best = lane_rule ? (((sub & 0xfff) << 3) | (sub >> 12)) : sub;
+        const int bm = max(best - 1, 0), bp = min(best + 1, D - 1);
+        auto elem = [&](int d) -> int {  // S[d & 7] of this lane
+            int v = S[0];
+#pragma unroll
+            for (int i = 1; i < 8; i++) v = (d & 7) == i ? S[i] : v;
+            return v;
+        };
+        const int Sm = __shfl(elem(bm), gbase + (bm >> 3), 64);
+        const int Sp = __shfl(elem(bp), gbase + (bp >> 3), 64);
+        bool rej = false;
+        if constexpr (UQ) {
+            int m2 = 0x7fffffff;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int d = d0 + i;
+                if (d < best - 1 || d > best + 1) m2 = min(m2, S[i]);
+            }
+#pragma unroll
+            for (int m = 1; m < LPP; m <<= 1) m2 = min(m2, __shfl_xor(m2, m, 64));
+            rej = m2 != 0x7fffffff && m2 * (100 - e.uniq) < minS * 100;
+        }
+        if (sl == 0 && xr < W1) {
+            const int bst = minS >= kMaxCost ? -1 : best;  // no strict minimum below MAX_COST
+            const int den = max(Sm + Sp - 2 * minS, 1);
+            const int frac = ((Sm - Sp) * kDispScale + den) / (den * 2);
+            const int d16 = bst * kDispScale + (frac & -(int)(0 < bst && bst < D - 1));
+            orow[x + minX1] = rej ? (int16_t)INV : (int16_t)(d16 + minD * kDispScale);
+            const int x2 = x + minX1 - bst - minD;
+            if (!rej && minS < kMaxCost && x2 >= 0 && x2 < W)
+                atomicMin(krow + x2, ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    // left-right check (src: OpenCV 3.4 final loop) -- reads the finished row
+    for (int x = minX1 + threadIdx.x; x < e.maxX1; x += kWtaThreads) {
+        const int v = orow[x];
+        if (v == INV) continue;
+        const int dlo = v >> kDispShift, dhi = (v + kDispScale - 1) >> kDispShift;
+        const int xl = x - dlo, xh = x - dhi;
+        auto d2at = [&](int xx) -> int {
+            const uint32_t k = __hip_atomic_load(krow + xx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k == 0xffffffffu) return INV;  // untouched: OpenCV's INVALID_DISP_SCALED
+            return 0xffff - (int)(k & 0xffffu) + minX1 - xx;
+        };
+        if (0 <= xl && xl < W && 0 <= xh && xh < W) {
+            const int a = d2at(xl), b = d2at(xh);
+            if (a >= minD && abs(a - dlo) > e.disp12 && b >= minD && abs(b - dhi) > e.disp12)
+                orow[x] = (int16_t)INV;
+        }
+    }
+}
+
 __global__ void fill_s16_kernel(int16_t* __restrict__ out, size_t os, size_t ofs, int W, int H,
                                 int16_t v)
 {
@@ -2023,6 +2172,17 @@ void launch_final16(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, const 
 // Every cost C = P2 + (box sum of blockSize^2 BT costs, each <= 2*ftzero + 63),
 // every L <= C and delta = minLp + P2: when that bound stays <= 32767 nothing
 // wraps in int16 and the path kernels may use the NW recurrence (sgm_pair).
+// The split side-by-side form (sgbm_wta_planes_kernel): byte / u16 planes,
+// D <= 32.  Measured (MI355X r06 sp2, split vs fused R->L + WTA): D 16 640x480
+// x 1 / 2 / 8 frames 0.278 -> 0.196, 0.297 -> 0.220, 0.515 -> 0.477 ms; D 32
+// 1280x960 0.522 -> 0.491; D 64 x 1 / 2 0.746 -> 0.802, 1.125 -> 1.282 and D 128
+// 1.083 -> 1.370 (the fifth chain set lengthens the direction pass more than
+// the chain-free WTA saves); MODE_HH D 64 1.01 either way
+static bool wta_split(const mvsv_ctx* ctx, const SgbmEff& e)
+{
+    return ctx->final_split && e.P2 > 15 && e.D <= 32;
+}
+
 static bool sgbm_no_wrap(const SgbmEff& e)
 {
     const long bs = 2L * e.SW2 + 1;
@@ -2398,12 +2558,16 @@ int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int1
 {
     static const int dirs_sgbm[4][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}};
     static const int dirs_hh[7][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}, {1, -1}, {0, -1}, {-1, -1}};
-    const int ndir = e.fullDP ? 7 : 4;
+    // split form: the R->L direction as one more chain set, the WTA on its own
+    constexpr bool kPlainPlanes = std::is_same<AccT, uint16_t>::value || std::is_same<AccT, uint8_t>::value;
+    const bool split = !RES && kPlainPlanes && wta_split(ctx, e);
+    const int ndir = (e.fullDP ? 7 : 4) + (split ? 1 : 0);
     PathDirs pd{};
     int maxnl = 0;
     for (int k = 0; k < ndir; k++) {
-        pd.dx[k] = e.fullDP ? dirs_hh[k][0] : dirs_sgbm[k][0];
-        pd.dy[k] = e.fullDP ? dirs_hh[k][1] : dirs_sgbm[k][1];
+        const bool rl = split && k == ndir - 1;
+        pd.dx[k] = rl ? -1 : e.fullDP ? dirs_hh[k][0] : dirs_sgbm[k][0];
+        pd.dy[k] = rl ? 0 : e.fullDP ? dirs_hh[k][1] : dirs_sgbm[k][1];
         maxnl = std::max(maxnl, num_lines(pd.dx[k], pd.dy[k], e.W1, H));
     }
     const size_t plane = (size_t)n * H * e.W1 * e.D;
@@ -2415,6 +2579,18 @@ int launch_paths_dirs(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int1
                            e.P1, e.P2);
     }
     StageTimer tm(ctx, kStageFinal);
+    if constexpr (kPlainPlanes) {
+        if (split) {
+            constexpr int LPP = 2 * NP * LPC / 8;  // D / 8
+            if (e.uniq > 0)
+                hipLaunchKernelGGL((sgbm_wta_planes_kernel<AccT, true, LPP>), dim3(H, n), dim3(kWtaThreads), 0,
+                                   ctx->stream, Cv, Av, plane, ndir, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
+            else
+                hipLaunchKernelGGL((sgbm_wta_planes_kernel<AccT, false, LPP>), dim3(H, n), dim3(kWtaThreads), 0,
+                                   ctx->stream, Cv, Av, plane, ndir, H, W, e, raw, (uint32_t*)ctx->keys.ptr);
+            return check_hip(ctx, hipGetLastError(), "sgbm path kernels (directions side by side, split WTA)");
+        }
+    }
     if (ndir == 7)
         launch_final16<NP, 7, AccT, NW, RES, LPC>(ctx, n, H, W, e, Cv, Av, plane, raw, Cin, Mv);
     else
@@ -2536,7 +2712,8 @@ int sgbm_device(mvsv_ctx* ctx, int n, const uint8_t* L, size_t ls, size_t lfs, c
     const bool bs = bsgm_eligible(ctx, e, n, H) && (sched == 1 || sched == 2) && ctx->path16 && ctx->tri &&
                     ctx->cost2 && ctx->cost_fixed_pp && e.SH2 <= 7 && e.SW2 == e.SH2;
     uint32_t* Bv = nullptr;
-    const int nplanes = sched == 2 ? (e.fullDP ? 7 : 4) : sched == 1 ? (e.fullDP ? 3 : 2) : 1;
+    const int nplanes = sched == 2 ? (e.fullDP ? 7 : 4) + (wta_split(ctx, e) ? 1 : 0)
+                                   : sched == 1 ? (e.fullDP ? 3 : 2) : 1;
     // 4-bit planes: one per direction (side by side, P2 <= 15) or per strip
     // pass + lines; bytes / u16 otherwise (side by side: one delta <= P2 each)
     const bool nib = (sched == 2 && e.P2 <= 15) || (sched == 1 && nplanes > 1 && acc_is_nib(e));

@@ -69,3 +69,58 @@ def test_d16_batch_matches_frames(gpu, mvsv, oracle, mode):
     for i in (0, 4, 7):
         want = oracle.sgbm(frames[i][0], frames[i][1], p)
         assert np.array_equal(out[i], want), f"frame {i}: " + report(out[i], want)
+
+
+@pytest.mark.parametrize("site", ["capture", "live"])
+def test_call_site_workspace_bound(gpu, mvsv, site):
+    """mvsv_sgbm_workspace_bytes bounds what a fresh context allocates for one frame of
+    the reference's call sites (directions side by side on u16 planes, R->L included)."""
+    import ctypes
+    from mvstereovision3_amd import _lib
+    torch = gpu
+    n, H, W = (1, 480, 640) if site == "capture" else (1, 960, 1280)
+    m = mvsv.StereoSGBM.create(0, 16, 5, 200, 800) if site == "capture" else \
+        mvsv.StereoSGBM.create(0, 64, 9, 648, 2592)
+    est = _lib.lib().mvsv_sgbm_workspace_bytes(n, W, H, ctypes.byref(m._params))
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5400)
+    L = torch.from_numpy(rng.integers(0, 256, (n, H, W), dtype=np.uint8)).to(dev)
+    R = torch.roll(L, -9, dims=2).contiguous()
+    out = torch.empty((n, H, W), dtype=torch.int16, device=dev)
+    torch.cuda.synchronize()
+    ctx = _lib.Context(0)
+    try:
+        free0 = torch.cuda.mem_get_info()[0]
+        with _lib.use_context(ctx):
+            m.compute(L, R, out)
+            _lib.synchronize(0)
+        used = free0 - torch.cuda.mem_get_info()[0]
+    finally:
+        ctx.close()
+    assert used <= est + (64 << 20), f"context used {used} B, workspace estimate {est} B"
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_call_sites_split_wta_both_forms(gpu, mvsv, oracle, split, monkeypatch):
+    """The side-by-side schedule on byte / u16 planes with the R->L direction as a chain
+    set and the per-pixel WTA kernel (MVSV_FINAL_SPLIT=1, default; D <= 32) and with the
+    fused R->L + WTA final kernel (0, and D > 32 either way): bit-exact, both modes,
+    uniqueness on and off, byte and u16 planes."""
+    from mvstereovision3_amd import _lib
+    monkeypatch.setenv("MVSV_FINAL_SPLIT", split)
+    ctx = _lib.Context(0)
+    try:
+        with _lib.use_context(ctx):
+            for i, (D, bs, P1, P2, uq, mode, W, H) in enumerate(
+                    [(16, 5, 200, 800, 0, 0, 320, 97), (64, 9, 648, 2592, 0, 0, 360, 64),
+                     (32, 7, 8, 40, 10, 1, 300, 51), (64, 5, 72, 300, 15, 1, 280, 40),
+                     (16, 3, 8, 20, 5, 0, 200, 33), (32, 3, 8, 30, 0, 1, 200, 33),
+                     (128, 9, 648, 2592, 10, 0, 420, 40)]):
+                L, R = mvsv.synth_pair(SEED0 + 180 + i, W, H, 0, D)
+                kw = dict(minDisparity=i - 2, numDisparities=D, blockSize=bs, P1=P1, P2=P2,
+                          uniquenessRatio=uq, disp12MaxDiff=1, speckleWindowSize=20, speckleRange=2, mode=mode)
+                for variant in (0, 2):
+                    got, want = sgbm_both(mvsv, oracle, L, R, variant=variant, **kw)
+                    assert np.array_equal(got, want), f"split={split} {kw} variant={variant}: " + report(got, want)
+    finally:
+        ctx.close()
