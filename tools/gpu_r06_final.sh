@@ -17,6 +17,7 @@ if [ "$2" != "--no-tests" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "tests failed"; tail -30 $O/gpu_tests.log; exit 1; }
 tail -1 $O/gpu_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; exit 1; }
+bash tools/gpu_census.sh $TAG/census || exit 1
 fi
 bash tools/sq_counters.sh $TAG/sq || exit 1
 python tools/sq_summary.py $O/sq $WL $O/sq_summary.json > $O/sq_summary.txt && cp $O/sq_summary.json $P/sq_summary.json || { echo "sq summary failed"; exit 1; }
