@@ -2441,7 +2441,12 @@ int launch_paths_tri(mvsv_ctx* ctx, int n, int H, int W, const SgbmEff& e, int16
             const int wv = ctx->strip_waves == wide || ctx->strip_waves == narrow
                                ? ctx->strip_waves
                                : (nblocks(wide) < ctx->cus ? narrow : wide);
-            aux_mode = 5 * nblocks(wv) <= 3 * ctx->cus ? 1 : (RES ? 2 : 0);
+            // Round 6: byte / u16 planes at D <= 64 run the lines beside the
+            // strips in batches too (liveDisparity default, 1280x960 x 4 / x 8:
+            // 1.97 -> 1.87, 3.13 -> 2.88 ms); D = 256 keeps them after the
+            // strips (x 4: 4.90 -> 5.7 ms beside, x 8: 8.60 -> 8.50;
+            // profiles/r06/aux/lines_aux_ab.txt)
+            aux_mode = 5 * nblocks(wv) <= 3 * ctx->cus ? 1 : ((RES || NP <= 2) ? 2 : 0);
         }
         hipStream_t ls = aux_mode ? ctx->aux : s;
         auto lines = [&]() {
